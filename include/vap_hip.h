@@ -1,0 +1,135 @@
+/* vap_hip.h -- C ABI of the MI355X-native VAP inference engine (libvap_hip.so).
+ *
+ * The reference (ErikEkstedt/VoiceActivityProjection) has no FFI: its boundary is the Python
+ * nn.Module API of vap/model.py.  These entry points are what that API binds to underneath
+ * (see INTEGRATION.md for the ctypes binding in voiceactivityprojection_amd/_native.py):
+ *
+ *   vap_create / vap_set_param / vap_finalize   <- VapGPT(conf) + load_state_dict(sd, strict=True)
+ *                                                  (vap/model.py:125-163, run.py:199-201)
+ *   vap_forward                                 <- VapGPT.forward(waveform)   (vap/model.py:249-268)
+ *   vap_probs + vap_labels_loss                 <- VapGPT.probs(waveform)     (vap/model.py:180-225)
+ *   vap_labels_loss                             <- ObjectiveVAP.get_labels + loss_vap (vap/objective.py:209-243)
+ *   vap_frame_lengths                           <- the conv length chain (vap/encoder_components.py:83-92,454-460)
+ *
+ * Conventions: plain pointers and sizes only.  Every tensor argument is a caller-allocated DEVICE
+ * buffer (float32 unless stated, C-contiguous).  `stream` is a hipStream_t passed as void*.
+ * All calls are asynchronous on `stream` except vap_timing_read.  Return value: VAP_OK or an
+ * error code; vap_last_error() gives a message (thread-local).  No global mutable state: one
+ * handle per model, reentrant across handles.
+ */
+#ifndef VAP_HIP_H
+#define VAP_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAP_OK 0
+#define VAP_ERR_INVALID 1     /* bad shape / argument (Python: AssertionError / ValueError) */
+#define VAP_ERR_TOO_SHORT 2   /* fewer than horizon+1 frames (Python: RuntimeError, quirk Q2) */
+#define VAP_ERR_HIP 3         /* HIP runtime failure */
+#define VAP_ERR_WEIGHTS 4     /* unknown key / wrong size / forward before finalize */
+#define VAP_ERR_UNSUPPORTED 5 /* configuration outside the kernels' specialisation */
+
+#define VAP_PRECISION_FP32 0  /* parity mode: fp32 storage, v_mfma_f32_16x16x4_f32 */
+#define VAP_PRECISION_BF16 1  /* perf mode: bf16 storage, v_mfma_f32_16x16x32_bf16, fp32 accumulate */
+
+/* kernel classes for vap_timing (HIP-event timing of one class inside the timed region) */
+#define VAP_K_CONV0 1
+#define VAP_K_CONV1 2
+#define VAP_K_CONV234 3
+#define VAP_K_LSTM_PROJ 4
+#define VAP_K_LSTM_REC 5
+#define VAP_K_DOWNSAMPLE 6
+#define VAP_K_TR_GEMM 7
+#define VAP_K_ATTN 8
+#define VAP_K_NORM 9
+#define VAP_K_HEADS 10
+#define VAP_K_PROBS 11
+
+typedef struct vap_dims {
+  int dim;            /* VapConfig.dim (must be 256: the CPC encoder width) */
+  int num_heads;      /* VapConfig.num_heads (head_dim must be 64) */
+  int channel_layers; /* VapConfig.channel_layers */
+  int cross_layers;   /* VapConfig.cross_layers */
+  int lstm_layers;    /* CPCAR nLevelsGRU (from the state dict) */
+  int n_bins;         /* len(VapConfig.bin_times) (must be 4: 256 classes) */
+  int precision;      /* VAP_PRECISION_* */
+} vap_dims;
+
+typedef struct vap_handle vap_handle;
+
+int vap_create(const vap_dims* dims, vap_handle** out);
+void vap_destroy(vap_handle* h);
+
+/* State-dict schema: parameter i has reference key `key` and `numel` float32 elements. */
+int vap_num_params(const vap_handle* h, int* n);
+int vap_param_info(const vap_handle* h, int i, const char** key, int64_t* numel);
+/* Copy one parameter (device fp32, reference layout) into the handle. */
+int vap_set_param(vap_handle* h, const char* key, const float* src, int64_t numel, void* stream);
+/* Repack every parameter into kernel layouts; required after the last vap_set_param. */
+int vap_finalize(vap_handle* h, void* stream);
+
+/* lens[0..5] = conv0..conv4 output lengths and the 50 Hz frame count T. */
+int vap_frame_lengths(int64_t n_samples, int64_t* lens);
+int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t* bytes);
+
+/* waveform [B][2][N] -> logits [B][T][256], vad_logits [B][T][2]. */
+int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
+                float* vad_logits, void* workspace, size_t workspace_bytes, void* stream);
+
+/* EncoderCPC.encode_audio (vap/model.py:169-175): out [2][B][T][256] = (x1, x2). */
+int vap_encode(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* out, void* workspace,
+               size_t workspace_bytes, void* stream);
+
+/* ObjectiveVAP.probs_next_speaker_aggregate (vap/objective.py:184-204): probs [B][T][256] -> out [B][T][2]. */
+int vap_aggregate(const float* probs, int batch, int frames, int n_bins, int from_bin, int to_bin, float* out,
+                  void* stream);
+
+/* VapGPT.vad post-processing (vap/model.py:227-247, vap/utils.py:239-272): binarise
+ * sigmoid(vad_logits [B][T][2]) >= cutoff, fill silences of <= max_fill_frames, then omit spikes of
+ * <= max_omit_frames -> out (0/1 floats). */
+int vap_vad_postprocess(const float* vad_logits, int batch, int frames, float cutoff, int max_fill_frames,
+                        int max_omit_frames, float* out, void* stream);
+
+/* probs() epilogue: probs [B][T][256], vad = sigmoid [B][T][2], p_now / p_future [B][T][2], H [B][T]. */
+int vap_probs(const float* logits, const float* vad_logits, int batch, int frames, int n_bins, int now0, int now1,
+              int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H, void* stream);
+
+/* labels [B][T - horizon] (int64) from voice activity va [B][T][2], and the per-frame VAP cross
+ * entropy loss [B][T - horizon] of logits [B][T][256] against them (logits and loss may both be
+ * NULL: labels only).  bin_frames is a HOST array of n_bins frame counts (bin_times_to_frames,
+ * vap/objective.py:10-11). */
+int vap_labels_loss(const float* logits, const float* va, int batch, int frames, const int* bin_frames, int n_bins,
+                    float threshold, int64_t* labels, float* loss, void* stream);
+
+/* Timing hook: record HIP events around every launch of kernel class `cls` (0 = off). */
+int vap_timing(vap_handle* h, int cls);
+/* Synchronises the recorded events; total device milliseconds and launch count since last read. */
+int vap_timing_read(vap_handle* h, double* total_ms, int* launches);
+
+const char* vap_last_error(void);
+const char* vap_build_info(void);
+
+/* ---- kernel-level test ABI (tests/test_gpu_kernels.py): each hot-path kernel on its own. ----
+ * Storage-type buffers are float (VAP_PRECISION_FP32) or bf16 (VAP_PRECISION_BF16). */
+int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, const void* W, int K, int N,
+                  const float* bias, int m_per_seq, int n_seq, void* C, int64_t ldc, int64_t c_seq, const float* add,
+                  int64_t ld_add, int64_t add_seq, const float* gamma, const float* beta, int norm, int act,
+                  int out_f32, void* stream);
+int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq, const void* K, int64_t k_ld,
+                       int64_t k_seq, const void* V, int64_t v_ld, int64_t v_seq, void* O, int64_t o_ld,
+                       int64_t o_seq, const float* slopes, int S, int T, int H, int kv_swap, float scale, void* stream);
+int vap_test_lstm(int precision, const float* gx, int S, int T, const float* whh, void* whh_packed, void* out,
+                  void* stream);
+int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
+                   const float* gamma, const float* beta, void* out, void* stream);
+int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
+                       void* raw, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,196 @@
+"""Kernel-level numerics: each HIP kernel (through the kernel test ABI of libvap_hip.so) against a
+plain PyTorch fp32 reference of the same op.  fp32 storage mode must agree to ~1e-5 relative
+(exact fp32 MFMA); bf16 storage mode is checked against the reference evaluated on the SAME
+bf16-rounded inputs (fp32 accumulate), so the tolerance only covers accumulation order and the
+bf16 rounding of the output."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+PREC = {"fp32": (0, torch.float32), "bf16": (1, torch.bfloat16)}
+
+
+def lib():
+    from voiceactivityprojection_amd import _native as N
+
+    return N
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _run(fn, *args):
+    N = lib()
+    N.check(fn(*args), fn.__name__)
+    torch.cuda.synchronize()
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", ["plain", "conv_cn_relu", "resid", "ln_gelu", "gelu"])
+def test_gemm(prec, case):
+    N = lib()
+    code, dt = PREC[prec]
+    g = torch.Generator().manual_seed(1)
+    if case == "plain":
+        S, Mps, K, Nn, lda = 1, 300, 256, 768, 256
+    elif case == "conv_cn_relu":
+        S, Mps, K, Nn, lda = 3, 77, 1024, 256, 512
+    elif case in ("resid", "gelu"):
+        S, Mps, K, Nn, lda = 2, 130, 768, 256, 768
+    else:
+        S, Mps, K, Nn, lda = 2, 201, 1280, 256, 512
+    L = (Mps - 1) * lda + K
+    A_flat = torch.randn(S, L, generator=g)
+    W = torch.randn(Nn, K, generator=g) / math.sqrt(K)
+    bias = torch.randn(Nn, generator=g) * 0.1
+    gamma = 1 + 0.2 * torch.randn(Nn, generator=g)
+    beta = 0.1 * torch.randn(Nn, generator=g)
+    add = torch.randn(S, Mps, Nn, generator=g)
+    Aq = A_flat.to(dt)
+    Wq = W.to(dt)
+    # reference on the (rounded) inputs
+    Ar, Wr = Aq.float(), Wq.float()
+    idx = torch.arange(Mps)[:, None] * lda + torch.arange(K)[None, :]
+    X = Ar[:, idx]  # (S, Mps, K) overlapping rows
+    ref = X @ Wr.T
+    norm = act = 0
+    use_bias = case != "plain"
+    use_add = case == "resid"
+    if use_bias:
+        ref = ref + bias
+    if case == "conv_cn_relu":
+        norm, act = 1, 1
+        mu = ref.mean(-1, keepdim=True)
+        var = ref.var(-1, keepdim=True)
+        ref = torch.relu((ref - mu) * torch.rsqrt(var + 1e-5) * gamma + beta)
+    elif case == "ln_gelu":
+        norm, act = 2, 2
+        ref = F.gelu(F.layer_norm(ref, (Nn,), gamma, beta))
+    elif case == "gelu":
+        act = 2
+        ref = F.gelu(ref)
+    if use_add:
+        ref = ref + add
+    out_f32 = 1 if (prec == "fp32" or case in ("resid", "ln_gelu")) else 0
+    C = torch.zeros(S, Mps, Nn, device="cuda", dtype=torch.float32 if out_f32 else dt)
+    Ad, Wd = Aq.cuda(), Wq.cuda()
+    bd, gd, bed, addd = bias.cuda(), gamma.cuda(), beta.cuda(), add.cuda()
+    _run(N.lib().vap_test_gemm, code, _p(Ad), lda, A_flat.shape[1], _p(Wd), K, Nn, _p(bd) if use_bias else None,
+         Mps, S, _p(C), Nn, Mps * Nn, _p(addd) if use_add else None, Nn, Mps * Nn, _p(gd), _p(bed), norm, act,
+         out_f32, _st())
+    got = C.float().cpu()
+    tol = 2e-4 if prec == "fp32" else (1e-2 if not out_f32 else 3e-3)
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= tol * max(1.0, scale), f"{prec}/{case}: max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("kv_swap", [0, 2])
+def test_attention(prec, kv_swap):
+    N = lib()
+    code, dt = PREC[prec]
+    g = torch.Generator().manual_seed(2)
+    S, T, H, D = 4, 150, 4, 256
+    Q = torch.randn(S, T, D, generator=g).to(dt)
+    K = torch.randn(S, T, D, generator=g).to(dt)
+    V = torch.randn(S, T, D, generator=g).to(dt)
+    slopes = torch.tensor([0.25, 0.0625, 0.015625, 0.00390625])
+    scale = 1 / 16
+    O = torch.zeros(S, T, D, device="cuda", dtype=dt)
+    Qd, Kd, Vd, sd = Q.cuda(), K.cuda(), V.cuda(), slopes.cuda()
+    _run(N.lib().vap_test_attention, code, _p(Qd), D, T * D, _p(Kd), D, T * D, _p(Vd), D, T * D, _p(O), D, T * D,
+         _p(sd), S, T, H, kv_swap, scale, _st())
+    kv = [(s + kv_swap) % S for s in range(S)]
+    q = Q.float().view(S, T, H, 64).transpose(1, 2)
+    k = K.float()[kv].view(S, T, H, 64).transpose(1, 2)
+    v = V.float()[kv].view(S, T, H, 64).transpose(1, 2)
+    att = torch.einsum("bhid,bhjd->bhij", q, k) * scale
+    bias = torch.arange(T).float().view(1, 1, 1, -1) * slopes.view(1, -1, 1, 1)
+    mask = torch.tril(torch.ones(T, T)) == 0
+    att = (att + bias).masked_fill(mask, float("-inf")).softmax(-1)
+    ref = (att @ v).transpose(1, 2).reshape(S, T, D)
+    err = (O.float().cpu() - ref).abs().max().item()
+    tol = 2e-5 if prec == "fp32" else 2e-2
+    assert err <= tol, f"{prec}: attention max err {err}"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_lstm(prec):
+    N = lib()
+    code, dt = PREC[prec]
+    g = torch.Generator().manual_seed(3)
+    S, T = 20, 37
+    gx = torch.randn(S, T, 1024, generator=g)
+    whh = (torch.rand(1024, 256, generator=g) * 2 - 1) / 16
+    out = torch.zeros(S, T, 256, device="cuda", dtype=dt)
+    packed = torch.zeros(1024 * 256, device="cuda", dtype=dt)
+    gxd, whd = gx.cuda(), whh.cuda()
+    _run(N.lib().vap_test_lstm, code, _p(gxd), S, T, _p(whd), _p(packed), _p(out), _st())
+    wr = whh.to(dt).float()
+    h = torch.zeros(S, 256)
+    c = torch.zeros(S, 256)
+    ys = []
+    for t in range(T):
+        z = gx[:, t] + h.to(dt).float() @ wr.T
+        i, f, gg, o = z.split(256, -1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        ys.append(h)
+    ref = torch.stack(ys, 1)
+    err = (out.float().cpu() - ref).abs().max().item()
+    tol = 2e-5 if prec == "fp32" else 1e-2
+    assert err <= tol, f"{prec}: lstm max err {err}"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv0(prec):
+    N = lib()
+    code, dt = PREC[prec]
+    g = torch.Generator().manual_seed(4)
+    B, n = 2, 3001
+    wav = torch.randn(B, 2, n, generator=g) * 0.1
+    w0 = torch.randn(256, 1, 10, generator=g) / math.sqrt(10)
+    b0 = torch.randn(256, generator=g) * 0.1
+    ga = 1 + 0.2 * torch.randn(256, generator=g)
+    be = 0.1 * torch.randn(256, generator=g)
+    L0 = (n + 6 - 10) // 5 + 1
+    out = torch.zeros(2 * B, L0 + 4, 256, device="cuda", dtype=dt)
+    d = [t.cuda() for t in (wav, w0, b0, ga, be)]
+    _run(N.lib().vap_test_conv0, code, _p(d[0]), B, n, L0, _p(d[1]), _p(d[2]), _p(d[3]), _p(d[4]), _p(out), _st())
+    x = torch.cat([wav[:, 0:1], wav[:, 1:2]], 0)  # channel-major sequences
+    y = F.conv1d(x, w0, b0, stride=5, padding=3)
+    mu, var = y.mean(1, keepdim=True), y.var(1, keepdim=True)
+    y = torch.relu((y - mu) * torch.rsqrt(var + 1e-5) * ga.view(1, -1, 1) + be.view(1, -1, 1)).transpose(1, 2)
+    got = out.float().cpu()[:, 2:L0 + 2]
+    err = (got - y).abs().max().item()
+    tol = 2e-5 if prec == "fp32" else 2e-2
+    assert err <= tol, f"{prec}: conv0 max err {err}"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_layernorm(prec):
+    N = lib()
+    code, dt = PREC[prec]
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(77, 256, generator=g) * 3 + 1
+    ga = 1 + 0.2 * torch.randn(256, generator=g)
+    be = 0.1 * torch.randn(256, generator=g)
+    out = torch.zeros(77, 256, device="cuda", dtype=dt)
+    raw = torch.zeros(77, 256, device="cuda", dtype=dt)
+    d = [t.cuda() for t in (x, ga, be)]
+    _run(N.lib().vap_test_layernorm, code, _p(d[0]), 77, _p(d[1]), _p(d[2]), _p(out), _p(raw), _st())
+    ref = F.layer_norm(x, (256,), ga, be)
+    tol = 1e-5 if prec == "fp32" else 2e-2
+    assert (out.float().cpu() - ref).abs().max().item() <= tol
+    assert (raw.float().cpu() - x.to(dt).float()).abs().max().item() == 0

@@ -1,0 +1,167 @@
+// Causal AliBi multi-head attention, flash style (no T x T score matrix in HBM).
+//
+// Reference: MultiHeadAttention.forward (vap/modules.py:82-110), AliBi bias/mask
+// (modules.py:169-202): score[h,i,j] = (q_i . k_j) * scale + m_h * j for j <= i, -inf above the
+// diagonal; scale = 1/sqrt(dim) (quirk Q5).  Softmax is shift-invariant per row, so the kernel
+// adds m_h * (j - i) (<= 0) instead of m_h * j: same probabilities, better conditioned in fp32.
+//
+// Work split: one workgroup = 64 queries of one (sequence, head); 4 waves x 16 queries.
+// S^T = K Q^T on the MFMA (A = K tile from LDS, B = Q from registers) puts each query on a lane
+// (col = lane & 15) so the online softmax is lane-local + 2 butterflies; O^T = V^T P^T takes P
+// straight from registers as the B operand (no P round trip through LDS; the k order inside a
+// k-step is permuted consistently on both operands).  V is staged transposed (V^T[d][key]).
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+constexpr int QB = 64, KB = 64, HDIM = 64;
+
+template <typename T>
+struct AttnGeom {
+  static constexpr int CE = 16 / sizeof(T);
+  static constexpr int CPR = HDIM / CE;                // 16-B chunks per K row (8 bf16, 16 f32)
+  static constexpr int KROW = HDIM * sizeof(T);        // 128 / 256 B
+  static constexpr int VROW = KB * sizeof(T) + (sizeof(T) == 2 ? 8 : 16);  // padded V^T row
+  static constexpr int KGD = HDIM / (4 * CE);          // k-groups over head dim (2 / 4)
+  VAP_DEV static int kswz(int row, int c) { return sizeof(T) == 2 ? (c ^ ((row >> 1) & 7)) : (c ^ (row & 15)); }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  using G = AttnGeom<T>;
+  __shared__ __attribute__((aligned(16))) unsigned char sk[KB * G::KROW];
+  __shared__ __attribute__((aligned(16))) unsigned char sv[HDIM * G::VROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int ks = (s + a.kv_swap) % a.S;
+  const T* Qs = (const T*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
+  const T* Ks = (const T*)a.K + (int64_t)ks * a.k_seq + h * HDIM;
+  const T* Vs = (const T*)a.V + (int64_t)ks * a.v_seq + h * HDIM;
+  const float slope = a.slopes[h];
+  const int q = qb * QB + w * 16 + (lane & 15);
+  const int qc = q < a.T ? q : a.T - 1;
+
+  chunk16 qf[G::KGD];
+#pragma unroll
+  for (int kg = 0; kg < G::KGD; ++kg)
+    qf[kg] = *(const chunk16*)(Qs + (int64_t)qc * a.q_ld + (kg * 4 + (lane >> 4)) * G::CE);
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb <= qb; ++kb) {
+    const int key0 = kb * KB;
+    // ---- stage K tile [key][d] (swizzled) and V^T tile [d][key]
+    for (int i = tid; i < KB * G::CPR; i += 256) {
+      const int row = i / G::CPR, c = i - row * G::CPR;
+      const int key = key0 + row;
+      chunk16 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+      if (key < a.T) {
+        kv = *(const chunk16*)(Ks + (int64_t)key * a.k_ld + c * G::CE);
+        vv = *(const chunk16*)(Vs + (int64_t)key * a.v_ld + c * G::CE);
+      }
+      *(chunk16*)(sk + row * G::KROW + G::kswz(row, c) * 16) = kv;
+      const T* ve = (const T*)&vv;
+#pragma unroll
+      for (int e = 0; e < G::CE; ++e) *(T*)(sv + (c * G::CE + e) * G::VROW + row * sizeof(T)) = ve[e];
+    }
+    __syncthreads();
+
+    // ---- S^T tiles: st[kt][r] = score(key = key0 + kt*16 + (lane>>4)*4 + r, query q)
+    f32x4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = kt * 16 + (lane & 15);
+#pragma unroll
+      for (int kg = 0; kg < G::KGD; ++kg) {
+        const chunk16 kf = *(const chunk16*)(sk + row * G::KROW + G::kswz(row, kg * 4 + (lane >> 4)) * 16);
+        acc = mfma_chunk<T>(kf, qf[kg], acc);
+      }
+      st[kt] = acc;
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = key0 + kt * 16 + (lane >> 4) * 4 + r;
+        float v = st[kt][r] * a.scale + slope * (float)(key - q);
+        if (key > q) v = -INFINITY;
+        st[kt][r] = v;
+        bm = fmaxf(bm, v);
+      }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = expf(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = expf(st[kt][r] - mn);
+        st[kt][r] = p;
+        ps += p;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+
+    // ---- O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const unsigned char* vrow = sv + (dt * 16 + (lane & 15)) * G::VROW;
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const u32x2 v0 = *(const u32x2*)(vrow + (32 * kk + (lane >> 4) * 4) * 2);
+          const u32x2 v1 = *(const u32x2*)(vrow + (32 * kk + 16 + (lane >> 4) * 4) * 2);
+          const chunk16 af = {v0.x, v0.y, v1.x, v1.y};
+          bf16x8 pb = {(bf16)st[2 * kk][0], (bf16)st[2 * kk][1], (bf16)st[2 * kk][2], (bf16)st[2 * kk][3],
+                       (bf16)st[2 * kk + 1][0], (bf16)st[2 * kk + 1][1], (bf16)st[2 * kk + 1][2],
+                       (bf16)st[2 * kk + 1][3]};
+          o[dt] = mfma_chunk<T>(af, __builtin_bit_cast(chunk16, pb), o[dt]);
+        }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const f32x4 vv = *(const f32x4*)(vrow + (kt * 16 + (lane >> 4) * 4) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[r], st[kt][r], o[dt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float lt = lsum + __shfl_xor(lsum, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  const float inv = 1.0f / lt;
+  if (q < a.T) {
+    T* orow = (T*)a.O + (int64_t)s * a.o_seq + (int64_t)q * a.o_ld + h * HDIM;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = dt * 16 + (lane >> 4) * 4;
+      store4(orow + d, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    }
+  }
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
+  if (a.T <= 0 || a.S <= 0 || a.H <= 0) return hipErrorInvalidValue;
+  dim3 grid((a.T + QB - 1) / QB, a.H, a.S);
+  hipLaunchKernelGGL((attn_kernel<T>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template hipError_t launch_attention<float>(const AttnArgs&, hipStream_t);
+template hipError_t launch_attention<bf16>(const AttnArgs&, hipStream_t);

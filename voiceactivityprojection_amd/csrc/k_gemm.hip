@@ -1,0 +1,242 @@
+// MFMA GEMM with implicit-convolution A addressing and fused row epilogues.
+//
+//   C[m, n] = epi( sum_k A[m, k] * W[n, k] )          (W = weight [N][K], K-contiguous)
+//   A row m = (seq s, frame t):  A + s*a_seq_stride + t*lda        (rows may OVERLAP: lda < K)
+//
+// Overlapping rows turn a strided Conv1d over a time-major [pos][ch] activation into a plain
+// GEMM with no im2col buffer:  conv k=8,s=4 (CPC conv1): lda = 4*256, K = 8*256;
+// conv k=4,s=2 (conv2..4): lda = 512, K = 1024; causal k=5,s=2 downsample: lda = 512, K = 1280
+// (reference: vap/encoder_components.py:83-92, 428-499).  Zero padding lives in explicit pad rows of
+// the activation buffers, so the loader never branches on the conv border.
+//
+// Epilogue (one code path, uniform runtime switches):
+//   v = acc + bias;  v = norm(v) [ChannelNorm: unbiased var (encoder_components.py:62-70) |
+//   LayerNorm: biased var (nn.LayerNorm)] * gamma + beta;  v = act(v) [relu | gelu(erf)];
+//   v += add (fp32 residual / combinator partial);  store as TOut.
+// Row norms need the whole 256-wide row in one workgroup: BN = 256.
+//
+// Tile 128 x 256, 8 waves (2 along M x 4 along N, 64x64 per wave = 4x4 MFMA 16x16 tiles),
+// K staged 128 bytes per row per step (64 bf16 / 32 f32) through a double-buffered, XOR-swizzled
+// LDS image (chunk ^= (row>>1)&7 : conflict-free ds_read_b128 for 16 consecutive rows).
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 256, ROWB = 128;  // bytes per staged row
+constexpr int BUF = (BM + BN) * ROWB;          // 48 KiB per stage
+
+VAP_DEV int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <typename T, typename TOut>
+__global__ __launch_bounds__(512) void gemm_kernel(GemmArgs g) {
+  constexpr int CE = 16 / sizeof(T);  // elements per 16-B chunk
+  constexpr int BK = 8 * CE;          // k per stage
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int M = g.M_per_seq * g.n_seq;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const T* __restrict__ A = (const T*)g.A;
+  const T* __restrict__ W = (const T*)g.W;
+
+  // ---- staging assignment: A 1024 chunks (2 / thread), B 2048 chunks (4 / thread)
+  const T* aptr[2];
+  bool aval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    const int m = m0 + row;
+    aval[i] = m < M;
+    const int mm = aval[i] ? m : 0;
+    const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
+    aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * CE;
+  }
+  const T* bptr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    bptr[i] = W + (int64_t)(n0 + row) * g.K + c * CE;
+  }
+  chunk16 ra[2], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + k0) : chunk16{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + k0);
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      *(chunk16*)(base + row * ROWB + swz(row, c) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      *(chunk16*)(base + BM * ROWB + row * ROWB + swz(row, c) * 16) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const unsigned char* abase = smem + cur * BUF;
+    const unsigned char* bbase = abase + BM * ROWB;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      chunk16 af[4], bfr[4];
+      const int c = sub * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + (lane & 15);
+        af[i] = *(const chunk16*)(abase + row * ROWB + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + (lane & 15);
+        bfr[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int colb = n0 + wn * 64 + (lane & 15);
+  if (g.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float b = g.bias[colb + j * 16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] += b;
+    }
+  }
+  if (g.norm) {
+    float* red = (float*)smem;  // [BM][4]
+    float mean[4][4], rstd[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = acc[i][0][r] + acc[i][1][r] + acc[i][2][r] + acc[i][3][r];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) red[rl * 4 + wn] = s;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const f32x4 p = *(const f32x4*)(red + rl * 4);
+        mean[i][r] = (p[0] + p[1] + p[2] + p[3]) * (1.0f / BN);
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = acc[i][j][r] - mean[i][r];
+          s += d * d;
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) red[rl * 4 + wn] = s;
+      }
+    __syncthreads();
+    const float inv_n = g.norm == 1 ? 1.0f / (BN - 1) : 1.0f / BN;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const f32x4 p = *(const f32x4*)(red + rl * 4);
+        const float var = (p[0] + p[1] + p[2] + p[3]) * inv_n;
+        rstd[i][r] = rsqrtf(var + g.eps);
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float ga = g.gamma[colb + j * 16], be = g.beta[colb + j * 16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = (acc[i][j][r] - mean[i][r]) * rstd[i][r] * ga + be;
+    }
+  }
+  if (g.act == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaxf(acc[i][j][r], 0.f);
+  } else if (g.act == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = gelu_erf(acc[i][j][r]);
+  }
+  TOut* __restrict__ C = (TOut*)g.C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+      TOut* crow = C + (int64_t)s * g.c_seq_stride + (int64_t)t * g.ldc;
+      const float* arow = g.add ? g.add + (int64_t)s * g.add_seq_stride + (int64_t)t * g.ld_add : nullptr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[i][j][r];
+        if (arow) v += arow[colb + j * 16];
+        crow[colb + j * 16] = from_f32<TOut>(v);
+      }
+    }
+}
+
+}  // namespace
+
+template <typename T, typename TOut>
+hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
+  const int M = g.M_per_seq * g.n_seq;
+  constexpr int BK = 8 * (16 / sizeof(T));
+  if (g.K % BK != 0 || g.N % BN != 0 || M <= 0) return hipErrorInvalidValue;
+  if (g.norm && g.N != BN) return hipErrorInvalidValue;
+  dim3 grid((M + BM - 1) / BM, g.N / BN);
+  hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);
+  return hipGetLastError();
+}
+
+template hipError_t launch_gemm<bf16, bf16>(const GemmArgs&, hipStream_t);
+template hipError_t launch_gemm<bf16, float>(const GemmArgs&, hipStream_t);
+template hipError_t launch_gemm<float, float>(const GemmArgs&, hipStream_t);

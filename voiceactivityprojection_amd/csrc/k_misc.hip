@@ -1,0 +1,397 @@
+// Memory-bound kernels of the VAP path: conv0 + ChannelNorm + ReLU, LayerNorm, the
+// va_classifier head, the probs() epilogue and label extraction + cross entropy.
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// conv0 (1 -> 256, k=10, s=5, p=3) -> ChannelNorm (unbiased var over 256 ch, eps 1e-5) -> ReLU
+// reference: vap/encoder_components.py:83-84 (conv0/batchNorm0), :62-70 (ChannelNorm), :99.
+// Block = 64 positions of one sequence; 4 threads per position, 64 channels each (registers),
+// row stats by two 4-lane butterflies.  Output time-major [seq][2 + L0 + 2][256] (2 pad rows
+// each side = conv1's zero padding).
+// ------------------------------------------------------------------------------------------
+constexpr int C0 = 256, KW0 = 10, WROW = 260;  // padded LDS row (bank spread across quarters)
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ wav, int B, int64_t N, int L0,
+                                                   const float* __restrict__ w0, const float* __restrict__ b0,
+                                                   const float* __restrict__ gam, const float* __restrict__ bet,
+                                                   T* __restrict__ out, int64_t out_seq_stride) {
+  __shared__ float sw[KW0 * WROW];
+  __shared__ float sb[3 * WROW];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C0 * KW0; i += 256) {
+    const int c = i / KW0, k = i - c * KW0;
+    sw[k * WROW + c + (c >> 6)] = w0[i];
+  }
+  {
+    const int c = tid;
+    sb[0 * WROW + c + (c >> 6)] = b0[c];
+    sb[1 * WROW + c + (c >> 6)] = gam[c];
+    sb[2 * WROW + c + (c >> 6)] = bet[c];
+  }
+  __syncthreads();
+  const int s = blockIdx.y;          // sequence = ch * B + b
+  const int ch = s / B, b = s - ch * B;
+  const int pos = blockIdx.x * 64 + (tid >> 2);
+  const int q = tid & 3;
+  if (pos >= L0) return;  // whole 4-lane groups exit together (shuffles stay within groups)
+  const float* src = wav + ((int64_t)b * 2 + ch) * N;
+  float smp[KW0];
+  const int64_t i0 = (int64_t)pos * 5 - 3;
+#pragma unroll
+  for (int k = 0; k < KW0; ++k) {
+    const int64_t i = i0 + k;
+    smp[k] = (i >= 0 && i < N) ? src[i] : 0.f;
+  }
+  float x[64];
+  float sum = 0.f;
+  const int cb = q * 64 + q;  // LDS column base incl. pad
+#pragma unroll
+  for (int cc = 0; cc < 64; ++cc) {
+    float v = sb[cb + cc];
+#pragma unroll
+    for (int k = 0; k < KW0; ++k) v = fmaf(sw[k * WROW + cb + cc], smp[k], v);
+    x[cc] = v;
+    sum += v;
+  }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
+  const float mean = sum * (1.0f / C0);
+  float ss = 0.f;
+#pragma unroll
+  for (int cc = 0; cc < 64; ++cc) {
+    const float d = x[cc] - mean;
+    ss += d * d;
+  }
+  ss += __shfl_xor(ss, 1, 64);
+  ss += __shfl_xor(ss, 2, 64);
+  const float rstd = rsqrtf(ss * (1.0f / (C0 - 1)) + 1e-5f);
+  T* o = out + (int64_t)s * out_seq_stride + (int64_t)(pos + 2) * C0 + q * 64;
+#pragma unroll
+  for (int cc = 0; cc < 64; cc += 4) {
+    float y[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v = (x[cc + e] - mean) * rstd * sb[WROW + cb + cc + e] + sb[2 * WROW + cb + cc + e];
+      y[e] = fmaxf(v, 0.f);
+    }
+    store4(o + cc, y[0], y[1], y[2], y[3]);
+  }
+}
+
+template <typename T>
+__global__ void zero_rows_kernel(T* base, int64_t seq_stride, int rows) {
+  const int s = blockIdx.y;
+  const int64_t n = (int64_t)rows * 256;
+  T* p = base + (int64_t)s * seq_stride;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = from_f32<T>(0.f);
+}
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm over 256 (nn.LayerNorm, biased var) -- one wave per row, 4 values per lane.
+// Optional raw copy (cross-attention K/V source is the UN-normalised x: modules.py:265-272).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, T* __restrict__ out, T* __restrict__ raw) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const f32x4 v = *(const f32x4*)(x + row * 256 + lane * 4);
+  if (raw) store4(raw + row * 256 + lane * 4, v[0], v[1], v[2], v[3]);
+  if (!gamma) return;
+  const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.0f / 256);
+  const f32x4 d = v - mean;
+  const float var = wave_sum(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) * (1.0f / 256);
+  const float rstd = rsqrtf(var + eps);
+  const f32x4 g = *(const f32x4*)(gamma + lane * 4);
+  const f32x4 b = *(const f32x4*)(beta + lane * 4);
+  const f32x4 y = d * rstd * g + b;
+  store4(out + row * 256 + lane * 4, y[0], y[1], y[2], y[3]);
+}
+
+// va_classifier (model.py:162,258-260): vad[b][t][c] = x_c[b,t] . w + bias; x rows fp32 channel-major
+__global__ __launch_bounds__(256) void vad_head_kernel(const float* __restrict__ x, int B, int Tn,
+                                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                                      float* __restrict__ vad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over (c, b, t)
+  const int64_t rows = (int64_t)2 * B * Tn;
+  if (row >= rows) return;
+  const f32x4 v = *(const f32x4*)(x + row * 256 + lane * 4);
+  const f32x4 ww = *(const f32x4*)(w + lane * 4);
+  const float d = wave_sum(v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3]) + bias[0];
+  if (lane == 0) {
+    const int64_t c = row / ((int64_t)B * Tn), bt = row - c * (int64_t)B * Tn;
+    vad[bt * 2 + c] = d;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// probs() epilogue (model.py:189-213): softmax, sigmoid VAD, entropy H = sum -p log2 p, and
+// probs_next_speaker_aggregate (objective.py:184-204) for the now / future bin ranges:
+//   abp[k, c] = popcount(bits of k in [c*nb+from, c*nb+to]);  p = probs . abp;  p /= sum_c p + 1e-5
+// One wave per frame, 4 classes per lane (n_classes = 256).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
+                                                   int64_t frames, int nb, int now0, int now1, int fut0, int fut1,
+                                                   float* __restrict__ probs, float* __restrict__ vad,
+                                                   float* __restrict__ p_now, float* __restrict__ p_future,
+                                                   float* __restrict__ H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= frames) return;
+  const f32x4 x = *(const f32x4*)(logits + f * 256 + lane * 4);
+  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+  f32x4 e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
+  const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
+  const f32x4 p = e / sum;
+  *(f32x4*)(probs + f * 256 + lane * 4) = p;
+  float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
+  const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
+  const unsigned mfut = ((1u << (fut1 - fut0 + 1)) - 1u) << fut0;
+  const unsigned bm = (1u << nb) - 1u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned k = lane * 4 + i;
+    h += -p[i] * log2f(p[i]);
+    const unsigned k0 = k & bm, k1 = (k >> nb) & bm;
+    n0 += p[i] * (float)__popc(k0 & mnow);
+    n1 += p[i] * (float)__popc(k1 & mnow);
+    u0 += p[i] * (float)__popc(k0 & mfut);
+    u1 += p[i] * (float)__popc(k1 & mfut);
+  }
+  h = wave_sum(h);
+  n0 = wave_sum(n0);
+  n1 = wave_sum(n1);
+  u0 = wave_sum(u0);
+  u1 = wave_sum(u1);
+  if (lane == 0) {
+    H[f] = h;
+    const float dn = n0 + n1 + 1e-5f, du = u0 + u1 + 1e-5f;
+    p_now[f * 2 + 0] = n0 / dn;
+    p_now[f * 2 + 1] = n1 / dn;
+    p_future[f * 2 + 0] = u0 / du;
+    p_future[f * 2 + 1] = u1 / du;
+    vad[f * 2 + 0] = 1.0f / (1.0f + expf(-vadl[f * 2 + 0]));
+    vad[f * 2 + 1] = 1.0f / (1.0f + expf(-vadl[f * 2 + 1]));
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// get_labels (objective.py:40-76,112-139; integer bit packing, bit-exact for binary VA) and
+// loss_vap(reduction='none') (objective.py:220-243) for frames t < T - horizon.
+// Lane j < 2*nb owns bit (c = j / nb, bin = j % nb): sequential fp32 window sum / len >= thr.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void labels_loss_kernel(const float* __restrict__ logits, const float* __restrict__ va,
+                                                         int B, int Tn, int nl, int4 bf, int nb, float thr,
+                                                         int64_t* __restrict__ labels, float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B * nl
+  if (f >= (int64_t)B * nl) return;
+  const int b = (int)(f / nl), t = (int)(f - (int64_t)b * nl);
+  const int bfr[4] = {bf.x, bf.y, bf.z, bf.w};
+  bool bit = false;
+  if (lane < 2 * nb) {
+    const int c = lane / nb, bin = lane - c * nb;
+    int start = 0;
+    for (int i = 0; i < bin; ++i) start += bfr[i];
+    const float* p = va + ((int64_t)b * Tn + t + 1 + start) * 2 + c;
+    float s = 0.f;
+    for (int j = 0; j < bfr[bin]; ++j) s += p[(int64_t)j * 2];
+    bit = (s / (float)bfr[bin]) >= thr;
+  }
+  const unsigned long long m = __ballot(bit);
+  // bit index of lane j = c*nb + bin == lane
+  const int64_t label = (int64_t)(m & ((1ull << (2 * nb)) - 1ull));
+  if (!logits) {
+    if (lane == 0) labels[f] = label;
+    return;
+  }
+  const float* lg = logits + ((int64_t)b * Tn + t) * 256;
+  const f32x4 x = *(const f32x4*)(lg + lane * 4);
+  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+  const float se = wave_sum(expf(x[0] - mx) + expf(x[1] - mx) + expf(x[2] - mx) + expf(x[3] - mx));
+  if (lane == 0) {
+    labels[f] = label;
+    loss[f] = (mx + logf(se)) - lg[label];
+  }
+}
+
+__global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict__ probs, int64_t frames, int nb,
+                                                       int from_bin, int to_bin, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= frames) return;
+  const f32x4 p = *(const f32x4*)(probs + f * 256 + lane * 4);
+  const unsigned msk = ((1u << (to_bin - from_bin + 1)) - 1u) << from_bin;
+  const unsigned bm = (1u << nb) - 1u;
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned k = lane * 4 + i;
+    a0 += p[i] * (float)__popc((k & bm) & msk);
+    a1 += p[i] * (float)__popc(((k >> nb) & bm) & msk);
+  }
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  if (lane == 0) {
+    const float d = a0 + a1 + 1e-5f;
+    out[f * 2 + 0] = a0 / d;
+    out[f * 2 + 1] = a1 / d;
+  }
+}
+
+// VapGPT.vad (model.py:227-247): sigmoid(vad logits) >= cutoff, then vad_fill_silences / vad_omit_spikes
+// (utils.py:239-272; islands via find_island_idx_len :21-49).  One thread per (batch, channel)
+// run-length scan; integer semantics, bit-exact.
+__global__ void vad_post_kernel(const float* __restrict__ vp, int B, int Tn, float cutoff, int max_fill, int max_omit,
+                                float* __restrict__ out) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= 2 * B) return;
+  const int b = id >> 1, c = id & 1;
+  const float* src = vp + (int64_t)b * Tn * 2 + c;
+  float* dst = out + (int64_t)b * Tn * 2 + c;
+  for (int t = 0; t < Tn; ++t) dst[(int64_t)t * 2] = (1.0f / (1.0f + expf(-src[(int64_t)t * 2]))) >= cutoff ? 1.f : 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float target = pass == 0 ? 0.f : 1.f;  // fill silences (0-runs), then omit spikes (1-runs)
+    const int lim = pass == 0 ? max_fill : max_omit;
+    int i = 0;
+    while (i < Tn) {
+      const float v = dst[(int64_t)i * 2];
+      int j = i + 1;
+      while (j < Tn && dst[(int64_t)j * 2] == v) ++j;
+      if (v == target && (j - i) <= lim)
+        for (int k = i; k < j; ++k) dst[(int64_t)k * 2] = 1.f - target;
+      i = j;
+    }
+  }
+}
+
+template <typename T>
+__global__ void convert_kernel(const float* in, T* out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = from_f32<T>(in[i]);
+}
+template <typename T>
+__global__ void pack_conv_kernel(const float* in, T* out, int N, int C, int KW) {
+  const int64_t n = (int64_t)N * C * KW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(i / ((int64_t)C * KW));
+    const int rem = (int)(i - (int64_t)o * C * KW);
+    const int c = rem / KW, j = rem - c * KW;
+    out[(int64_t)o * C * KW + (int64_t)j * C + c] = from_f32<T>(in[i]);
+  }
+}
+__global__ void add_vec_kernel(const float* a, const float* b, float* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_conv0(const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
+                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st) {
+  dim3 grid((L0 + 63) / 64, 2 * B);
+  hipLaunchKernelGGL((conv0_kernel<T>), grid, dim3(256), 0, st, wav, B, N, L0, w0, b0, gamma, beta, out,
+                     out_seq_stride);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_zero_rows(T* base, int n_seq, int64_t seq_stride, int rows, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t n = (int64_t)rows * 256;
+  dim3 grid((unsigned)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64), n_seq);
+  hipLaunchKernelGGL((zero_rows_kernel<T>), grid, dim3(256), 0, st, base, seq_stride, rows);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_layernorm(const float* x, int64_t rows, const float* gamma, const float* beta, float eps, T* out,
+                            T* raw, hipStream_t st) {
+  hipLaunchKernelGGL((layernorm_kernel<T>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, rows, gamma, beta,
+                     eps, out, raw);
+  return hipGetLastError();
+}
+
+hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const float* bias, float* vad,
+                           hipStream_t st) {
+  const int64_t rows = (int64_t)2 * B * Tn;
+  hipLaunchKernelGGL(vad_head_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, B, Tn, w, bias, vad);
+  return hipGetLastError();
+}
+
+hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
+                        int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,
+                        hipStream_t st) {
+  const int64_t frames = (int64_t)B * Tn;
+  hipLaunchKernelGGL(probs_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, logits, vad_logits, frames,
+                     n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_labels_loss(const float* logits, const float* va, int B, int Tn, const int* bin_frames, int n_bins,
+                              float threshold, int64_t* labels, float* loss, hipStream_t st) {
+  if (n_bins < 1 || n_bins > 4) return hipErrorInvalidValue;
+  int horizon = 0;
+  int4 bf = {0, 0, 0, 0};
+  int* bp = &bf.x;
+  for (int i = 0; i < n_bins; ++i) {
+    bp[i] = bin_frames[i];
+    horizon += bin_frames[i];
+  }
+  const int nl = Tn - horizon;
+  if (nl <= 0) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * nl;
+  hipLaunchKernelGGL(labels_loss_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, logits, va, B, Tn, nl, bf,
+                     n_bins, threshold, labels, loss);
+  return hipGetLastError();
+}
+
+hipError_t launch_aggregate(const float* probs, int64_t frames, int nb, int from_bin, int to_bin, float* out,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, probs, frames, nb, from_bin,
+                     to_bin, out);
+  return hipGetLastError();
+}
+hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, int max_fill, int max_omit, float* out,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(vad_post_kernel, dim3((2 * B + 63) / 64), dim3(64), 0, st, vad_probs, B, Tn, cutoff, max_fill,
+                     max_omit, out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_convert(const float* in, T* out, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL((convert_kernel<T>), dim3(256), dim3(256), 0, st, in, out, n);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t launch_pack_conv(const float* in, T* out, int N, int C, int KW, hipStream_t st) {
+  hipLaunchKernelGGL((pack_conv_kernel<T>), dim3(256), dim3(256), 0, st, in, out, N, C, KW);
+  return hipGetLastError();
+}
+hipError_t launch_add_vec(const float* a, const float* b, float* out, int n, hipStream_t st) {
+  hipLaunchKernelGGL(add_vec_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, b, out, n);
+  return hipGetLastError();
+}
+
+#define INST(T)                                                                                                       \
+  template hipError_t launch_conv0<T>(const float*, int, int64_t, int, const float*, const float*, const float*,       \
+                                      const float*, T*, int64_t, hipStream_t);                                         \
+  template hipError_t launch_zero_rows<T>(T*, int, int64_t, int, hipStream_t);                                          \
+  template hipError_t launch_layernorm<T>(const float*, int64_t, const float*, const float*, float, T*, T*,           \
+                                          hipStream_t);                                                                \
+  template hipError_t launch_convert<T>(const float*, T*, int64_t, hipStream_t);                                      \
+  template hipError_t launch_pack_conv<T>(const float*, T*, int, int, int, hipStream_t);
+INST(float)
+INST(bf16)

@@ -1,0 +1,74 @@
+// Shared device helpers for the VAP MI355X engine (gfx950 / CDNA4 only).
+//
+// Precision model: "storage" type T feeds the matrix cores.
+//   T = __bf16 : perf mode, v_mfma_f32_16x16x32_bf16 (fp32 accumulate)
+//   T = float  : parity mode, v_mfma_f32_16x16x4_f32 (exact fp32 fmaf chain)
+// Both share one fragment geometry: every lane reads 16 contiguous bytes of a K-contiguous
+// row ([row][k] layout) -- 8 bf16 (one 16x16x32 MFMA) or 4 floats (four 16x16x4 MFMAs covering
+// k-slots (lane>>4) with k = 4*(lane>>4)+j).  Accumulator (C/D) layout for both:
+//   col = lane & 15, row = (lane >> 4) * 4 + r,  r = 0..3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+#define VAP_DEV __device__ __forceinline__
+
+VAP_DEV float to_f32(float x) { return x; }
+VAP_DEV float to_f32(bf16 x) { return (float)x; }
+template <typename T> VAP_DEV T from_f32(float x);
+template <> VAP_DEV float from_f32<float>(float x) { return x; }
+template <> VAP_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// 16-byte fragment chunk: 8 bf16 or 4 floats.
+typedef u32x4 chunk16;
+
+// One "16-byte k-chunk" MFMA step: acc += A_chunk(row=lane&15) x B_chunk(col=lane&15).
+// bf16: 16x16x32 (chunk = k 8*(lane>>4)..+7 of a 32-wide k-step)
+// f32 : 4 x 16x16x4 (chunk = k 4*(lane>>4)..+3 of a 16-wide k-step)
+template <typename T> VAP_DEV f32x4 mfma_chunk(chunk16 a, chunk16 b, f32x4 acc);
+template <> VAP_DEV f32x4 mfma_chunk<bf16>(chunk16 a, chunk16 b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
+                                                 0, 0, 0);
+}
+// NOTE: bit-cast the WHOLE vector.  hipcc (ROCm 7.2 clang) lowers __builtin_bit_cast(float, v[i]) on
+// an ext_vector element to a load of element 0 whatever i is (verified in the .ll / .s).
+template <> VAP_DEV f32x4 mfma_chunk<float>(chunk16 a, chunk16 b, f32x4 acc) {
+  const f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], acc, 0, 0, 0);
+  return acc;
+}
+
+// elements of T per 16-byte chunk
+template <typename T> struct ChunkElems { static constexpr int v = 16 / sizeof(T); };
+
+VAP_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+VAP_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// wave64 butterfly sums over lane bits [lo, hi)
+VAP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+VAP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// store 4 consecutive values as T
+VAP_DEV void store4(float* p, float a, float b, float c, float d) { *(f32x4*)p = f32x4{a, b, c, d}; }
+VAP_DEV void store4(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  *(bf16x4*)p = v;
+}

@@ -1,0 +1,701 @@
+// Host side of the MI355X VAP engine: parameter store + packing, workspace planning and the
+// forward orchestration of VapGPT.forward (vap/model.py:249-268) over HIP kernels.
+// Exposes the C ABI declared in include/vap_hip.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/vap_hip.h"
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      return fail(VAP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
+  } while (0)
+
+constexpr int D = 256;
+
+struct Param {
+  int64_t numel = 0;
+  float* dev = nullptr;
+  bool set = false;
+};
+
+}  // namespace
+
+struct vap_handle {
+  vap_dims dims{};
+  std::vector<std::string> keys;
+  std::map<std::string, Param> params;
+  std::map<std::string, void*> packed;  // storage-type buffers
+  std::map<std::string, float*> fpacked;  // fp32 derived buffers (e.g. summed LSTM biases)
+  bool finalized = false;
+  // timing hook
+  int timing_cls = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t ev_used = 0;
+
+  ~vap_handle() {
+    for (auto& kv : params) (void)hipFree(kv.second.dev);
+    for (auto& kv : packed) (void)hipFree(kv.second);
+    for (auto& kv : fpacked) (void)hipFree(kv.second);
+    for (auto& e : ev) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+  }
+  const float* P(const std::string& k) const { return params.at(k).dev; }
+  template <typename T>
+  const T* W(const std::string& k) const { return (const T*)packed.at(k); }
+};
+
+namespace {
+
+void add_schema(vap_handle* h) {
+  auto add = [&](const std::string& k, int64_t n) {
+    h->keys.push_back(k);
+    h->params[k].numel = n;
+  };
+  const vap_dims& d = h->dims;
+  const std::string g = "encoder.encoder.gEncoder";
+  const int kws[5] = {10, 8, 4, 4, 4};
+  for (int i = 0; i < 5; ++i) {
+    const int cin = i == 0 ? 1 : D;
+    add(g + ".conv" + std::to_string(i) + ".weight", (int64_t)D * cin * kws[i]);
+    add(g + ".conv" + std::to_string(i) + ".bias", D);
+    add(g + ".batchNorm" + std::to_string(i) + ".weight", D);
+    add(g + ".batchNorm" + std::to_string(i) + ".bias", D);
+  }
+  for (int l = 0; l < d.lstm_layers; ++l) {
+    const std::string p = "encoder.encoder.gAR.baseNet.", s = "_l" + std::to_string(l);
+    add(p + "weight_ih" + s, 4 * D * D);
+    add(p + "weight_hh" + s, 4 * D * D);
+    add(p + "bias_ih" + s, 4 * D);
+    add(p + "bias_hh" + s, 4 * D);
+  }
+  add("encoder.downsample.1.weight", D * D * 5);
+  add("encoder.downsample.1.bias", D);
+  add("encoder.downsample.2.ln.weight", D);
+  add("encoder.downsample.2.ln.bias", D);
+  auto layer = [&](const std::string& p, bool cross) {
+    add(p + ".ln_self_attn.weight", D);
+    add(p + ".ln_self_attn.bias", D);
+    add(p + ".ln_ffnetwork.weight", D);
+    add(p + ".ln_ffnetwork.bias", D);
+    add(p + ".mha.m", d.num_heads);
+    for (const char* n : {"key", "query", "value", "proj"}) add(p + ".mha." + n + ".weight", D * D);
+    add(p + ".ffnetwork.0.weight", 3 * D * D);
+    add(p + ".ffnetwork.3.weight", 3 * D * D);
+    if (cross) {
+      add(p + ".ln_src_attn.weight", D);
+      add(p + ".ln_src_attn.bias", D);
+      add(p + ".mha_cross.m", d.num_heads);
+      for (const char* n : {"key", "query", "value", "proj"}) add(p + ".mha_cross." + n + ".weight", D * D);
+    }
+  };
+  for (int l = 0; l < d.channel_layers; ++l) layer("ar_channel.layers." + std::to_string(l), false);
+  for (int l = 0; l < d.cross_layers; ++l) layer("ar.layers." + std::to_string(l), true);
+  add("ar.combinator.h0_a.weight", D * D);
+  add("ar.combinator.h0_b.weight", D * D);
+  add("ar.combinator.ln.weight", D);
+  add("ar.combinator.ln.bias", D);
+  add("objective.codebook.emb.weight", 256 * 8);
+  add("va_classifier.weight", D);
+  add("va_classifier.bias", 1);
+  add("vap_head.weight", 256 * D);
+  add("vap_head.bias", 256);
+}
+
+int64_t conv_len(int64_t n, int k, int s, int pl, int pr) {
+  const int64_t v = n + pl + pr - k;
+  return v < 0 ? 0 : v / s + 1;
+}
+
+void frame_lengths(int64_t n, int64_t* L) {
+  L[0] = conv_len(n, 10, 5, 3, 3);
+  L[1] = conv_len(L[0], 8, 4, 2, 2);
+  L[2] = conv_len(L[1], 4, 2, 1, 1);
+  L[3] = conv_len(L[2], 4, 2, 1, 1);
+  L[4] = conv_len(L[3], 4, 2, 1, 1);
+  L[5] = conv_len(L[4], 5, 2, 4, 0);
+}
+
+// ------------------------------------------------------------------------ workspace plan
+struct Plan {
+  int B = 0, S = 0, T = 0;
+  int64_t L[6]{};
+  int64_t s0, s1, s2, s3, s4, sh;  // per-sequence strides (elements) of padded activations
+  size_t X0, X1, X2, X3, X4, GX, H0, H1, X, LN, RAW, QKV, KVC, QC, ATT, FF, HC, HCT, total;
+};
+
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+Plan make_plan(int B, int64_t N, size_t es) {
+  Plan p;
+  p.B = B;
+  p.S = 2 * B;
+  frame_lengths(N, p.L);
+  p.T = (int)p.L[5];
+  const int64_t S = p.S, T = p.T;
+  p.s0 = (p.L[0] + 4) * D;
+  p.s1 = (p.L[1] + 2) * D;
+  p.s2 = (p.L[2] + 2) * D;
+  p.s3 = (p.L[3] + 2) * D;
+  p.s4 = (p.L[4] + 2) * D;
+  p.sh = (p.L[4] + 4) * D;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t r = o;
+    o = align_up(o + bytes);
+    return r;
+  };
+  p.X0 = take(S * p.s0 * es);
+  p.X1 = take(S * p.s1 * es);
+  p.X2 = take(S * p.s2 * es);
+  p.X3 = take(S * p.s3 * es);
+  p.X4 = take(S * p.s4 * es);
+  p.GX = take(S * p.L[4] * 4 * D * sizeof(float));
+  p.H0 = take(S * p.sh * es);
+  p.H1 = take(S * p.sh * es);
+  p.X = take(S * T * D * sizeof(float));
+  p.LN = take(S * T * D * es);
+  p.RAW = take(S * T * D * es);
+  p.QKV = take(S * T * 3 * D * es);
+  p.KVC = take(S * T * 2 * D * es);
+  p.QC = take(S * T * D * es);
+  p.ATT = take(S * T * D * es);
+  p.FF = take(S * T * 3 * D * es);
+  p.HC = take((size_t)B * T * D * sizeof(float));
+  p.HCT = take((size_t)B * T * D * es);
+  p.total = o;
+  return p;
+}
+
+// ------------------------------------------------------------------------ timing hook
+struct Timed {
+  vap_handle* h;
+  hipStream_t st;
+  bool on;
+  size_t idx = 0;
+  Timed(vap_handle* hh, int cls, hipStream_t s) : h(hh), st(s), on(hh->timing_cls != 0 && hh->timing_cls == cls) {
+    if (!on) return;
+    if (h->ev_used == h->ev.size()) {
+      hipEvent_t a, b;
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      h->ev.push_back({a, b});
+    }
+    idx = h->ev_used++;
+    (void)hipEventRecord(h->ev[idx].first, st);
+  }
+  ~Timed() {
+    if (on) (void)hipEventRecord(h->ev[idx].second, st);
+  }
+};
+
+template <typename T>
+hipError_t gemm(const GemmArgs& g, hipStream_t st, bool out_f32) {
+  if (out_f32) return launch_gemm<T, float>(g, st);
+  if constexpr (sizeof(T) == 2) return launch_gemm<bf16, bf16>(g, st);
+  return launch_gemm<float, float>(g, st);
+}
+
+GemmArgs gargs(const void* A, int64_t lda, int64_t aseq, const void* W, int K, int N, const float* bias, int Mps, int nseq,
+               void* C, int64_t ldc, int64_t cseq) {
+  GemmArgs g{};
+  g.A = A;
+  g.lda = lda;
+  g.a_seq_stride = aseq;
+  g.W = W;
+  g.K = K;
+  g.N = N;
+  g.bias = bias;
+  g.M_per_seq = Mps;
+  g.n_seq = nseq;
+  g.C = C;
+  g.ldc = ldc;
+  g.c_seq_stride = cseq;
+  g.eps = 1e-5f;
+  return g;
+}
+
+// ------------------------------------------------------------------------ packing
+template <typename T>
+int pack_all(vap_handle* h, hipStream_t st) {
+  auto alloc = [&](const std::string& name, int64_t n) -> T* {
+    void* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
+    h->packed[name] = p;
+    return (T*)p;
+  };
+  const std::string g = "encoder.encoder.gEncoder";
+  const int kws[5] = {10, 8, 4, 4, 4};
+  for (int i = 1; i < 5; ++i) {
+    T* w = alloc("conv" + std::to_string(i), (int64_t)D * D * kws[i]);
+    if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv");
+    HIPCHK(launch_pack_conv<T>(h->P(g + ".conv" + std::to_string(i) + ".weight"), w, D, D, kws[i], st));
+  }
+  for (int l = 0; l < h->dims.lstm_layers; ++l) {
+    const std::string p = "encoder.encoder.gAR.baseNet.", s = "_l" + std::to_string(l);
+    T* wih = alloc("wih" + s, 4 * D * D);
+    T* whh = alloc("whh" + s, 4 * D * D);
+    float* b = nullptr;
+    if (!wih || !whh || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
+    h->fpacked["bias" + s] = b;
+    HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
+    HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
+    HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
+  }
+  {
+    T* w = alloc("down", D * D * 5);
+    if (!w) return fail(VAP_ERR_HIP, "hipMalloc down");
+    HIPCHK(launch_pack_conv<T>(h->P("encoder.downsample.1.weight"), w, D, D, 5, st));
+  }
+  auto cat = [&](const std::string& name, std::vector<std::string> srcs) -> int {
+    int64_t total = 0;
+    for (auto& k : srcs) total += h->params.at(k).numel;
+    T* w = alloc(name, total);
+    if (!w) return fail(VAP_ERR_HIP, "hipMalloc " + name);
+    int64_t off = 0;
+    for (auto& k : srcs) {
+      const Param& pr = h->params.at(k);
+      HIPCHK(launch_convert<T>(pr.dev, w + off, pr.numel, st));
+      off += pr.numel;
+    }
+    return VAP_OK;
+  };
+  auto layer = [&](const std::string& p, bool cross) -> int {
+    int rc;
+    if ((rc = cat(p + ".qkv", {p + ".mha.query.weight", p + ".mha.key.weight", p + ".mha.value.weight"}))) return rc;
+    if ((rc = cat(p + ".o", {p + ".mha.proj.weight"}))) return rc;
+    if ((rc = cat(p + ".w1", {p + ".ffnetwork.0.weight"}))) return rc;
+    if ((rc = cat(p + ".w2", {p + ".ffnetwork.3.weight"}))) return rc;
+    if (cross) {
+      if ((rc = cat(p + ".qc", {p + ".mha_cross.query.weight"}))) return rc;
+      if ((rc = cat(p + ".kvc", {p + ".mha_cross.key.weight", p + ".mha_cross.value.weight"}))) return rc;
+      if ((rc = cat(p + ".oc", {p + ".mha_cross.proj.weight"}))) return rc;
+    }
+    return VAP_OK;
+  };
+  int rc;
+  for (int l = 0; l < h->dims.channel_layers; ++l)
+    if ((rc = layer("ar_channel.layers." + std::to_string(l), false))) return rc;
+  for (int l = 0; l < h->dims.cross_layers; ++l)
+    if ((rc = layer("ar.layers." + std::to_string(l), true))) return rc;
+  if ((rc = cat("comb_a", {"ar.combinator.h0_a.weight"}))) return rc;
+  if ((rc = cat("comb_b", {"ar.combinator.h0_b.weight"}))) return rc;
+  if ((rc = cat("head", {"vap_head.weight"}))) return rc;
+  return VAP_OK;
+}
+
+// ------------------------------------------------------------------------ forward
+template <typename T>
+int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, hipStream_t st) {
+  const int S = p.S, T_ = p.T;
+  const int64_t rows = (int64_t)S * T_;
+  float* X = (float*)(ws + p.X);
+  T* LN = (T*)(ws + p.LN);
+  T* RAW = (T*)(ws + p.RAW);
+  T* QKV = (T*)(ws + p.QKV);
+  T* KVC = (T*)(ws + p.KVC);
+  T* QC = (T*)(ws + p.QC);
+  T* ATT = (T*)(ws + p.ATT);
+  T* FF = (T*)(ws + p.FF);
+  const int H = h->dims.num_heads;
+  const float scale = 1.0f / std::sqrt((float)D);
+  const bool f32out = false;
+  {
+    Timed tm(h, VAP_K_NORM, st);
+    HIPCHK(launch_layernorm<T>(X, rows, h->P(pre + ".ln_self_attn.weight"), h->P(pre + ".ln_self_attn.bias"), 1e-5f, LN,
+                               cross ? RAW : nullptr, st));
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(gemm<T>(gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".qkv"), D, 3 * D, nullptr, T_, S, QKV, 3 * D,
+                         (int64_t)T_ * 3 * D), st, f32out));
+    if (cross)
+      HIPCHK(gemm<T>(gargs(RAW, D, (int64_t)T_ * D, h->W<T>(pre + ".kvc"), D, 2 * D, nullptr, T_, S, KVC, 2 * D,
+                           (int64_t)T_ * 2 * D), st, f32out));
+  }
+  {
+    Timed tm(h, VAP_K_ATTN, st);
+    AttnArgs a{QKV, 3 * D, (int64_t)T_ * 3 * D, QKV + D, 3 * D, (int64_t)T_ * 3 * D, QKV + 2 * D, 3 * D,
+               (int64_t)T_ * 3 * D, ATT, D, (int64_t)T_ * D, h->P(pre + ".mha.m"), S, T_, H, 0, scale};
+    HIPCHK(launch_attention<T>(a, st));
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    GemmArgs g = gargs(ATT, D, (int64_t)T_ * D, h->W<T>(pre + ".o"), D, D, nullptr, T_, S, X, D, (int64_t)T_ * D);
+    g.add = X;
+    g.ld_add = D;
+    g.add_seq_stride = (int64_t)T_ * D;
+    HIPCHK(gemm<T>(g, st, true));
+  }
+  if (cross) {
+    {
+      Timed tm(h, VAP_K_NORM, st);
+      HIPCHK(launch_layernorm<T>(X, rows, h->P(pre + ".ln_src_attn.weight"), h->P(pre + ".ln_src_attn.bias"), 1e-5f, LN,
+                                 nullptr, st));
+    }
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      HIPCHK(gemm<T>(gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".qc"), D, D, nullptr, T_, S, QC, D, (int64_t)T_ * D),
+                     st, f32out));
+    }
+    {
+      Timed tm(h, VAP_K_ATTN, st);
+      AttnArgs a{QC, D, (int64_t)T_ * D, KVC, 2 * D, (int64_t)T_ * 2 * D, KVC + D, 2 * D, (int64_t)T_ * 2 * D,
+                 ATT, D, (int64_t)T_ * D, h->P(pre + ".mha_cross.m"), S, T_, H, p.B, scale};
+      HIPCHK(launch_attention<T>(a, st));
+    }
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      GemmArgs g = gargs(ATT, D, (int64_t)T_ * D, h->W<T>(pre + ".oc"), D, D, nullptr, T_, S, X, D, (int64_t)T_ * D);
+      g.add = X;
+      g.ld_add = D;
+      g.add_seq_stride = (int64_t)T_ * D;
+      HIPCHK(gemm<T>(g, st, true));
+    }
+  }
+  {
+    Timed tm(h, VAP_K_NORM, st);
+    HIPCHK(launch_layernorm<T>(X, rows, h->P(pre + ".ln_ffnetwork.weight"), h->P(pre + ".ln_ffnetwork.bias"), 1e-5f, LN,
+                               nullptr, st));
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    GemmArgs g = gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".w1"), D, 3 * D, nullptr, T_, S, FF, 3 * D,
+                       (int64_t)T_ * 3 * D);
+    g.act = 2;
+    HIPCHK(gemm<T>(g, st, f32out));
+    GemmArgs g2 = gargs(FF, 3 * D, (int64_t)T_ * 3 * D, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D,
+                        (int64_t)T_ * D);
+    g2.add = X;
+    g2.ld_add = D;
+    g2.add_seq_stride = (int64_t)T_ * D;
+    HIPCHK(gemm<T>(g2, st, true));
+  }
+  return VAP_OK;
+}
+
+template <typename T>
+int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits, float* vadl, unsigned char* ws,
+                hipStream_t st, float* enc_out = nullptr) {
+  const Plan p = make_plan(B, N, sizeof(T));
+  const int S = p.S, T_ = p.T;
+  const int64_t* L = p.L;
+  T* X0 = (T*)(ws + p.X0);
+  T* X1 = (T*)(ws + p.X1);
+  T* X2 = (T*)(ws + p.X2);
+  T* X3 = (T*)(ws + p.X3);
+  T* X4 = (T*)(ws + p.X4);
+  float* GX = (float*)(ws + p.GX);
+  T* Hb[2] = {(T*)(ws + p.H0), (T*)(ws + p.H1)};
+  float* X = (float*)(ws + p.X);
+  const std::string g = "encoder.encoder.gEncoder";
+
+  // pad rows (conv zero padding lives in explicit rows)
+  HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
+  HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
+  T* Xs[4] = {X1, X2, X3, X4};
+  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
+  for (int i = 0; i < 4; ++i) {
+    HIPCHK(launch_zero_rows<T>(Xs[i], S, ss[i], 1, st));
+    HIPCHK(launch_zero_rows<T>(Xs[i] + (L[i + 1] + 1) * D, S, ss[i], 1, st));
+  }
+  HIPCHK(launch_zero_rows<T>(Hb[0], S, p.sh, 4, st));
+  HIPCHK(launch_zero_rows<T>(Hb[1], S, p.sh, 4, st));
+
+  {  // conv0 + CN0 + ReLU  (encoder_components.py:99)
+    Timed tm(h, VAP_K_CONV0, st);
+    HIPCHK(launch_conv0<T>(wav, B, N, (int)L[0], h->P(g + ".conv0.weight"), h->P(g + ".conv0.bias"),
+                           h->P(g + ".batchNorm0.weight"), h->P(g + ".batchNorm0.bias"), X0, p.s0, st));
+  }
+  // conv1..conv4 as implicit GEMMs with ChannelNorm + ReLU epilogue (encoder_components.py:100-103)
+  const T* ins[4] = {X0, X1, X2, X3};
+  const int64_t in_ss[4] = {p.s0, p.s1, p.s2, p.s3};
+  const int lda[4] = {4 * D, 2 * D, 2 * D, 2 * D};
+  const int Ks[4] = {8 * D, 4 * D, 4 * D, 4 * D};
+  for (int i = 0; i < 4; ++i) {
+    const std::string c = std::to_string(i + 1);
+    Timed tm(h, i == 0 ? VAP_K_CONV1 : VAP_K_CONV234, st);
+    GemmArgs ga = gargs(ins[i], lda[i], in_ss[i], h->W<T>("conv" + c), Ks[i], D, h->P(g + ".conv" + c + ".bias"),
+                        (int)L[i + 1], S, Xs[i] + D, D, ss[i]);
+    ga.norm = 1;
+    ga.act = 1;
+    ga.gamma = h->P(g + ".batchNorm" + c + ".weight");
+    ga.beta = h->P(g + ".batchNorm" + c + ".bias");
+    HIPCHK(gemm<T>(ga, st, false));
+  }
+  // LSTM (encoder_components.py:140-159): input projection GEMM + serial recurrence per layer
+  const int NL = h->dims.lstm_layers;
+  for (int l = 0; l < NL; ++l) {
+    const std::string s = "_l" + std::to_string(l);
+    const T* in = l == 0 ? X4 + D : Hb[(l - 1) & 1] + 4 * D;
+    const int64_t in_seq = l == 0 ? p.s4 : p.sh;
+    {
+      Timed tm(h, VAP_K_LSTM_PROJ, st);
+      HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L[4], S, GX,
+                           4 * D, L[4] * 4 * D), st, true));
+    }
+    {
+      Timed tm(h, VAP_K_LSTM_REC, st);
+      HIPCHK(launch_lstm<T>(GX, S, (int)L[4], h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, st));
+    }
+  }
+  {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
+    Timed tm(h, VAP_K_DOWNSAMPLE, st);
+    GemmArgs ga = gargs(Hb[(NL - 1) & 1], 2 * D, p.sh, h->W<T>("down"), 5 * D, D, h->P("encoder.downsample.1.bias"), T_,
+                        S, X, D, (int64_t)T_ * D);
+    ga.norm = 2;
+    ga.act = 2;
+    ga.gamma = h->P("encoder.downsample.2.ln.weight");
+    ga.beta = h->P("encoder.downsample.2.ln.bias");
+    HIPCHK(gemm<T>(ga, st, true));
+  }
+  if (enc_out) {  // EncoderCPC output of both speakers, [2][B][T][256] (channel-major)
+    HIPCHK(hipMemcpyAsync(enc_out, X, (size_t)S * T_ * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return VAP_OK;
+  }
+  int rc;
+  for (int l = 0; l < h->dims.channel_layers; ++l)
+    if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, st))) return rc;
+  for (int l = 0; l < h->dims.cross_layers; ++l)
+    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, st))) return rc;
+
+  // combinator (modules.py:434-449) + heads (model.py:257-261)
+  T* RAW = (T*)(ws + p.RAW);
+  float* HC = (float*)(ws + p.HC);
+  T* HCT = (T*)(ws + p.HCT);
+  {
+    Timed tm(h, VAP_K_HEADS, st);
+    HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
+    GemmArgs ga = gargs(RAW, D, (int64_t)T_ * D, h->W<T>("comb_a"), D, D, nullptr, T_, B, HC, D, (int64_t)T_ * D);
+    ga.norm = 2;
+    ga.act = 2;
+    ga.gamma = h->P("ar.combinator.ln.weight");
+    ga.beta = h->P("ar.combinator.ln.bias");
+    HIPCHK(gemm<T>(ga, st, true));
+    GemmArgs gb = ga;
+    gb.A = RAW + (int64_t)B * T_ * D;
+    gb.W = h->W<T>("comb_b");
+    gb.add = HC;
+    gb.ld_add = D;
+    gb.add_seq_stride = (int64_t)T_ * D;
+    HIPCHK(gemm<T>(gb, st, true));
+    HIPCHK(launch_layernorm<T>(HC, (int64_t)B * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
+    HIPCHK(gemm<T>(gargs(HCT, D, (int64_t)T_ * D, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, B, logits, 256,
+                         (int64_t)T_ * 256), st, true));
+    HIPCHK(launch_vad_head(X, B, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"), vadl, st));
+  }
+  return VAP_OK;
+}
+
+}  // namespace
+
+// ============================================================================== C ABI
+extern "C" {
+
+const char* vap_last_error(void) { return g_err.c_str(); }
+
+const char* vap_build_info(void) {
+  return "libvap_hip gfx950 kernels: conv0-cn, mfma-gemm(implicit conv, row-norm epilogue), lstm-mfma, "
+         "flash-attn-alibi, probs, labels";
+}
+
+int vap_create(const vap_dims* dims, vap_handle** out) {
+  if (!dims || !out) return fail(VAP_ERR_INVALID, "null argument");
+  if (dims->dim != D) return fail(VAP_ERR_UNSUPPORTED, "dim must be 256 (CPC encoder width)");
+  if (dims->num_heads <= 0 || D % dims->num_heads || D / dims->num_heads != 64)
+    return fail(VAP_ERR_UNSUPPORTED, "head_dim must be 64 (num_heads = 4)");
+  if (dims->n_bins != 4) return fail(VAP_ERR_UNSUPPORTED, "n_bins must be 4 (256 VAP classes)");
+  if (dims->lstm_layers < 1 || dims->channel_layers < 0 || dims->cross_layers < 0)
+    return fail(VAP_ERR_INVALID, "bad layer counts");
+  if (dims->precision != VAP_PRECISION_FP32 && dims->precision != VAP_PRECISION_BF16)
+    return fail(VAP_ERR_INVALID, "bad precision");
+  vap_handle* h = new vap_handle();
+  h->dims = *dims;
+  add_schema(h);
+  for (auto& kv : h->params) {
+    if (hipMalloc(&kv.second.dev, kv.second.numel * sizeof(float)) != hipSuccess) {
+      delete h;
+      return fail(VAP_ERR_HIP, "hipMalloc params");
+    }
+  }
+  *out = h;
+  return VAP_OK;
+}
+
+void vap_destroy(vap_handle* h) { delete h; }
+
+int vap_num_params(const vap_handle* h, int* n) {
+  if (!h || !n) return fail(VAP_ERR_INVALID, "null argument");
+  *n = (int)h->keys.size();
+  return VAP_OK;
+}
+
+int vap_param_info(const vap_handle* h, int i, const char** key, int64_t* numel) {
+  if (!h || i < 0 || i >= (int)h->keys.size()) return fail(VAP_ERR_INVALID, "param index out of range");
+  if (key) *key = h->keys[i].c_str();
+  if (numel) *numel = h->params.at(h->keys[i]).numel;
+  return VAP_OK;
+}
+
+int vap_set_param(vap_handle* h, const char* key, const float* src, int64_t numel, void* stream) {
+  if (!h || !key || !src) return fail(VAP_ERR_INVALID, "null argument");
+  auto it = h->params.find(key);
+  if (it == h->params.end()) return fail(VAP_ERR_WEIGHTS, std::string("unexpected key: ") + key);
+  if (it->second.numel != numel)
+    return fail(VAP_ERR_WEIGHTS, std::string("size mismatch for ") + key + ": expected " +
+                                     std::to_string(it->second.numel) + " got " + std::to_string(numel));
+  HIPCHK(hipMemcpyAsync(it->second.dev, src, numel * sizeof(float), hipMemcpyDefault, (hipStream_t)stream));
+  it->second.set = true;
+  h->finalized = false;
+  return VAP_OK;
+}
+
+int vap_finalize(vap_handle* h, void* stream) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  for (auto& k : h->keys)
+    if (!h->params.at(k).set) return fail(VAP_ERR_WEIGHTS, "missing key: " + k);
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  for (auto& kv : h->packed) (void)hipFree(kv.second);
+  for (auto& kv : h->fpacked) (void)hipFree(kv.second);
+  h->packed.clear();
+  h->fpacked.clear();
+  const int rc = h->dims.precision == VAP_PRECISION_BF16 ? pack_all<bf16>(h, (hipStream_t)stream)
+                                                          : pack_all<float>(h, (hipStream_t)stream);
+  if (rc) return rc;
+  const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return fail(VAP_ERR_HIP, std::string("weight packing: ") + hipGetErrorString(e));
+  h->finalized = true;
+  return VAP_OK;
+}
+
+int vap_frame_lengths(int64_t n_samples, int64_t* lens) {
+  if (!lens || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad n_samples");
+  frame_lengths(n_samples, lens);
+  return VAP_OK;
+}
+
+int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t* bytes) {
+  if (!h || !bytes || batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad argument");
+  int64_t L[6];
+  frame_lengths(n_samples, L);
+  if (L[5] <= 0) return fail(VAP_ERR_INVALID, "waveform too short for one frame");
+  *bytes = make_plan(batch, n_samples, h->dims.precision == VAP_PRECISION_BF16 ? 2 : 4).total;
+  return VAP_OK;
+}
+
+int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits, float* vad_logits,
+                void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h || !waveform || !logits || !vad_logits || !workspace) return fail(VAP_ERR_INVALID, "null argument");
+  if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
+  if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  size_t need = 0;
+  int rc = vap_workspace_size(h, batch, n_samples, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) return fail(VAP_ERR_INVALID, "workspace too small: need " + std::to_string(need));
+  return h->dims.precision == VAP_PRECISION_BF16
+             ? run_forward<bf16>(h, waveform, batch, n_samples, logits, vad_logits, (unsigned char*)workspace,
+                                 (hipStream_t)stream)
+             : run_forward<float>(h, waveform, batch, n_samples, logits, vad_logits, (unsigned char*)workspace,
+                                  (hipStream_t)stream);
+}
+
+int vap_encode(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* out, void* workspace,
+               size_t workspace_bytes, void* stream) {
+  if (!h || !waveform || !out || !workspace) return fail(VAP_ERR_INVALID, "null argument");
+  if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
+  if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  size_t need = 0;
+  int rc = vap_workspace_size(h, batch, n_samples, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) return fail(VAP_ERR_INVALID, "workspace too small: need " + std::to_string(need));
+  return h->dims.precision == VAP_PRECISION_BF16
+             ? run_forward<bf16>(h, waveform, batch, n_samples, nullptr, nullptr, (unsigned char*)workspace,
+                                 (hipStream_t)stream, out)
+             : run_forward<float>(h, waveform, batch, n_samples, nullptr, nullptr, (unsigned char*)workspace,
+                                  (hipStream_t)stream, out);
+}
+
+int vap_aggregate(const float* probs, int batch, int frames, int n_bins, int from_bin, int to_bin, float* out,
+                  void* stream) {
+  if (!probs || !out) return fail(VAP_ERR_INVALID, "null argument");
+  if (n_bins != 4) return fail(VAP_ERR_UNSUPPORTED, "n_bins must be 4");
+  if (from_bin < 0 || to_bin < from_bin || to_bin >= n_bins) return fail(VAP_ERR_INVALID, "bad bin limits");
+  HIPCHK(launch_aggregate(probs, (int64_t)batch * frames, n_bins, from_bin, to_bin, out, (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_vad_postprocess(const float* vad_logits, int batch, int frames, float cutoff, int max_fill_frames,
+                        int max_omit_frames, float* out, void* stream) {
+  if (!vad_logits || !out || batch <= 0 || frames <= 0) return fail(VAP_ERR_INVALID, "bad argument");
+  HIPCHK(launch_vad_post(vad_logits, batch, frames, cutoff, max_fill_frames, max_omit_frames, out, (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_probs(const float* logits, const float* vad_logits, int batch, int frames, int n_bins, int now0, int now1,
+              int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H, void* stream) {
+  if (!logits || !vad_logits || !probs || !vad || !p_now || !p_future || !H) return fail(VAP_ERR_INVALID, "null argument");
+  if (n_bins != 4) return fail(VAP_ERR_UNSUPPORTED, "n_bins must be 4");
+  if (now0 < 0 || now1 < now0 || now1 >= n_bins || fut0 < 0 || fut1 < fut0 || fut1 >= n_bins)
+    return fail(VAP_ERR_INVALID, "bad bin limits");
+  HIPCHK(launch_probs(logits, vad_logits, batch, frames, n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H,
+                      (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_labels_loss(const float* logits, const float* va, int batch, int frames, const int* bin_frames, int n_bins,
+                    float threshold, int64_t* labels, float* loss, void* stream) {
+  if (!va || !bin_frames || !labels || (logits && !loss)) return fail(VAP_ERR_INVALID, "null argument");
+  if (n_bins != 4) return fail(VAP_ERR_UNSUPPORTED, "n_bins must be 4");
+  int horizon = 0;
+  for (int i = 0; i < n_bins; ++i) horizon += bin_frames[i];
+  if (frames - 1 < horizon)
+    return fail(VAP_ERR_TOO_SHORT, "maximum size for tensor at dimension 1 is " + std::to_string(frames - 1) +
+                                       " but size is " + std::to_string(horizon));
+  HIPCHK(launch_labels_loss(logits, va, batch, frames, bin_frames, n_bins, threshold, labels, loss, (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_timing(vap_handle* h, int cls) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  h->timing_cls = cls;
+  h->ev_used = 0;
+  return VAP_OK;
+}
+
+int vap_timing_read(vap_handle* h, double* total_ms, int* launches) {
+  if (!h || !total_ms || !launches) return fail(VAP_ERR_INVALID, "null argument");
+  double tot = 0.0;
+  for (size_t i = 0; i < h->ev_used; ++i) {
+    HIPCHK(hipEventSynchronize(h->ev[i].second));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->ev[i].first, h->ev[i].second));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = (int)h->ev_used;
+  h->ev_used = 0;
+  return VAP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// Internal launch interface between the engine (vap_engine.cpp) and the kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct GemmArgs {
+  const void* A;          // storage type T
+  int64_t lda;            // row stride (elements); may be < K for implicit conv
+  int64_t a_seq_stride;   // per-sequence stride (elements)
+  const void* W;          // [N][K] storage type T
+  int K, N;
+  const float* bias;      // [N] or null
+  int M_per_seq, n_seq;   // M = M_per_seq * n_seq
+  void* C;                // TOut
+  int64_t ldc, c_seq_stride;
+  const float* add;       // fp32 addend (may alias C when TOut == float) or null
+  int64_t ld_add, add_seq_stride;
+  const float* gamma;     // norm affine (N == 256)
+  const float* beta;
+  float eps;
+  int norm;               // 0 none, 1 ChannelNorm (unbiased var), 2 LayerNorm (biased var)
+  int act;                // 0 none, 1 relu, 2 gelu(erf)
+};
+
+template <typename T, typename TOut>
+hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+
+// conv0 (1 -> 256, k10 s5 p3) + ChannelNorm + ReLU, time-major output with pad rows.
+template <typename T>
+hipError_t launch_conv0(const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
+                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st);
+
+// Zero `rows` rows of width 256 at `base + s*seq_stride` for every sequence (pad rows).
+template <typename T>
+hipError_t launch_zero_rows(T* base, int n_seq, int64_t seq_stride, int rows, hipStream_t st);
+
+// LayerNorm over 256 (biased var) of fp32 rows -> T, optional raw fp32->T copy.
+template <typename T>
+hipError_t launch_layernorm(const float* x, int64_t rows, const float* gamma, const float* beta, float eps,
+                            T* out, T* raw, hipStream_t st);
+
+// LSTM recurrence.  gx: [S][T][4H] fp32 (x W_ih^T + b_ih + b_hh), whh_packed: fragment-ordered
+// W_hh (storage T), out: T rows with stride out_seq_stride, h (256) per row.
+template <typename T>
+hipError_t launch_lstm(const float* gx, int S, int Tn, const T* whh_packed, T* out, int64_t out_seq_stride,
+                       hipStream_t st);
+template <typename T>
+hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st);
+
+struct AttnArgs {
+  const void* Q; int64_t q_ld, q_seq;     // head h at column h*64
+  const void* K; int64_t k_ld, k_seq;
+  const void* V; int64_t v_ld, v_seq;
+  void* O; int64_t o_ld, o_seq;
+  const float* slopes;                    // [H]
+  int S, T, H;
+  int kv_swap;                            // K/V sequence = (s + kv_swap) % S  (0 = self)
+  float scale;
+};
+template <typename T>
+hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
+
+// va_classifier on both towers: vad[b][t][c] = dot(x_c[b,t], w) + bias (x fp32, channel-major seqs)
+hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const float* bias, float* vad, hipStream_t st);
+
+hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
+                        int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,
+                        hipStream_t st);
+hipError_t launch_labels_loss(const float* logits, const float* va, int B, int Tn, const int* bin_frames, int n_bins,
+                              float threshold, int64_t* labels, float* loss, hipStream_t st);
+
+// fp32 -> storage conversion (weights packing) and small helpers
+template <typename T>
+hipError_t launch_convert(const float* in, T* out, int64_t n, hipStream_t st);
+// out[n][j*C + c] = in[n][c][j]  (conv weight (N, C, KW) -> K-contiguous (tap, channel) order)
+template <typename T>
+hipError_t launch_pack_conv(const float* in, T* out, int N, int C, int KW, hipStream_t st);
+hipError_t launch_add_vec(const float* a, const float* b, float* out, int n, hipStream_t st);
+
+// probs_next_speaker_aggregate on a probs tensor [frames][256] -> out [frames][2]
+hipError_t launch_aggregate(const float* probs, int64_t frames, int nb, int from_bin, int to_bin, float* out,
+                            hipStream_t st);
+// VapGPT.vad post-processing: (p >= cutoff) -> fill silences <= max_fill -> omit spikes <= max_omit
+hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, int max_fill, int max_omit, float* out,
+                           hipStream_t st);

@@ -1,0 +1,104 @@
+// Kernel-level test ABI: every hot-path kernel callable on its own, so tests/test_gpu_kernels.py
+// can check each one against a plain PyTorch fp32 reference of the same op.  Not used by the
+// engine itself.  precision: VAP_PRECISION_FP32 (storage float) / VAP_PRECISION_BF16 (storage bf16).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/vap_hip.h"
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+int rc_of(hipError_t e) { return e == hipSuccess ? VAP_OK : VAP_ERR_HIP; }
+}  // namespace
+
+namespace {
+// one v_mfma_f32_16x16x4_f32 with lane-provided operands: d[lane][r]
+__global__ void probe_mfma_f32(const float* a, const float* b, float* d) {
+  const int l = threadIdx.x;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[l], b[l], acc, 0, 0, 0);
+  for (int r = 0; r < 4; ++r) d[l * 4 + r] = acc[r];
+}
+}  // namespace
+
+extern "C" {
+
+int vap_test_probe_mfma_f32(const float* a, const float* b, float* d, void* stream) {
+  hipLaunchKernelGGL(probe_mfma_f32, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, d);
+  return rc_of(hipGetLastError());
+}
+
+int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, const void* W, int K, int N,
+                  const float* bias, int m_per_seq, int n_seq, void* C, int64_t ldc, int64_t c_seq, const float* add,
+                  int64_t ld_add, int64_t add_seq, const float* gamma, const float* beta, int norm, int act,
+                  int out_f32, void* stream) {
+  GemmArgs g{};
+  g.A = A;
+  g.lda = lda;
+  g.a_seq_stride = a_seq;
+  g.W = W;
+  g.K = K;
+  g.N = N;
+  g.bias = bias;
+  g.M_per_seq = m_per_seq;
+  g.n_seq = n_seq;
+  g.C = C;
+  g.ldc = ldc;
+  g.c_seq_stride = c_seq;
+  g.add = add;
+  g.ld_add = ld_add;
+  g.add_seq_stride = add_seq;
+  g.gamma = gamma;
+  g.beta = beta;
+  g.eps = 1e-5f;
+  g.norm = norm;
+  g.act = act;
+  hipStream_t st = (hipStream_t)stream;
+  if (precision == VAP_PRECISION_BF16)
+    return rc_of(out_f32 ? launch_gemm<bf16, float>(g, st) : launch_gemm<bf16, bf16>(g, st));
+  return rc_of(launch_gemm<float, float>(g, st));
+}
+
+int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq, const void* K, int64_t k_ld,
+                       int64_t k_seq, const void* V, int64_t v_ld, int64_t v_seq, void* O, int64_t o_ld,
+                       int64_t o_seq, const float* slopes, int S, int T, int H, int kv_swap, float scale, void* stream) {
+  AttnArgs a{Q, q_ld, q_seq, K, k_ld, k_seq, V, v_ld, v_seq, O, o_ld, o_seq, slopes, S, T, H, kv_swap, scale};
+  hipStream_t st = (hipStream_t)stream;
+  return rc_of(precision == VAP_PRECISION_BF16 ? launch_attention<bf16>(a, st) : launch_attention<float>(a, st));
+}
+
+// whh_packed: scratch of 1024*256 storage elements; out: [S][T][256] storage type
+int vap_test_lstm(int precision, const float* gx, int S, int T, const float* whh, void* whh_packed, void* out,
+                  void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (precision == VAP_PRECISION_BF16) {
+    hipError_t e = launch_pack_whh<bf16>(whh, (bf16*)whh_packed, st);
+    if (e != hipSuccess) return VAP_ERR_HIP;
+    return rc_of(launch_lstm<bf16>(gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st));
+  }
+  hipError_t e = launch_pack_whh<float>(whh, (float*)whh_packed, st);
+  if (e != hipSuccess) return VAP_ERR_HIP;
+  return rc_of(launch_lstm<float>(gx, S, T, (const float*)whh_packed, (float*)out, (int64_t)T * 256, st));
+}
+
+// out: [2B][L0 + 4][256] storage type (pad rows untouched)
+int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
+                   const float* gamma, const float* beta, void* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t seq = (int64_t)(L0 + 4) * 256;
+  if (precision == VAP_PRECISION_BF16)
+    return rc_of(launch_conv0<bf16>(wav, B, N, L0, w0, b0, gamma, beta, (bf16*)out, seq, st));
+  return rc_of(launch_conv0<float>(wav, B, N, L0, w0, b0, gamma, beta, (float*)out, seq, st));
+}
+
+int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
+                       void* raw, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (precision == VAP_PRECISION_BF16)
+    return rc_of(launch_layernorm<bf16>(x, rows, gamma, beta, 1e-5f, (bf16*)out, (bf16*)raw, st));
+  return rc_of(launch_layernorm<float>(x, rows, gamma, beta, 1e-5f, (float*)out, (float*)raw, st));
+}
+
+}  // extern "C"

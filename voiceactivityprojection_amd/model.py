@@ -1,0 +1,315 @@
+"""Drop-in mirror of the reference model API (vap/model.py) on the MI355X engine.
+
+    from vap.model import VapGPT, VapConfig, VAPModel, load_older_state_dict, BIN_TIMES
+
+* ``VapConfig``      == vap/model.py:42-79 (same fields, same ``--vap_*`` argparse flags).
+* ``VapGPT``         == vap/model.py:125-268: same module tree / state-dict keys (``load_state_dict``
+  with ``strict=True`` as run.py:199-201), same ``forward`` / ``probs`` / ``vad`` / ``encode_audio``
+  signatures, outputs and errors.  Parameters live in ordinary torch Parameters (storage only);
+  all compute runs in ``libvap_hip.so`` through the C ABI (include/vap_hip.h).  CPU tensors raise:
+  there is no CPU fallback.
+* ``VAPModel``       the reference's Lightning training class name (vap/train.py:244), exported
+  here as an inference-only alias of VapGPT.
+
+Extra (engine) knobs: ``precision`` ("fp32" parity mode, default; "bf16" perf mode) as a
+constructor argument / ``VAP_PRECISION`` env var, and ``lstm_layers`` (inferred from state dicts).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from . import _native as N
+from .objective import ObjectiveVAP
+from .weights import schema as _schema
+from .weights import synthetic_state_dict
+
+BIN_TIMES: list = [0.2, 0.4, 0.6, 0.8]
+
+
+def load_older_state_dict(path="example/VAP_3mmz3t0u_50Hz_ad20s_134-epoch9-val_2.56.ckpt"):
+    """vap/model.py:28-39 (old Lightning checkpoint key remap); safe loader only."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)["state_dict"]
+    new_sd = {}
+    for k, v in sd.items():
+        if "VAP.codebook" in k:
+            continue
+        if "vap_head" in k:
+            k = k.replace("vap_head.projection_head", "vap_head")
+        new_sd[k.replace("net.", "")] = v
+    return new_sd
+
+
+@dataclass
+class VapConfig:
+    sample_rate: int = 16_000
+    frame_hz: int = 50
+    bin_times: List[float] = field(default_factory=lambda: BIN_TIMES)
+
+    # Encoder (training flag)
+    freeze_encoder: int = 1
+    load_pretrained: int = 1
+
+    # GPT
+    dim: int = 256
+    channel_layers: int = 1
+    cross_layers: int = 3
+    num_heads: int = 4
+    dropout: float = 0.1
+
+    @staticmethod
+    def add_argparse_args(parser, fields_added=[]):
+        for k, v in VapConfig.__dataclass_fields__.items():
+            if k == "bin_times":
+                parser.add_argument(f"--vap_{k}", nargs="+", type=float, default=v.default_factory())
+            else:
+                parser.add_argument(f"--vap_{k}", type=v.type, default=v.default)
+            fields_added.append(k)
+        return parser, fields_added
+
+    @staticmethod
+    def args_to_conf(args):
+        return VapConfig(**{k.replace("vap_", ""): v for k, v in vars(args).items() if k.startswith("vap_")})
+
+
+def _container(root: nn.Module, dotted: str) -> nn.Module:
+    mod = root
+    for part in dotted.split("."):
+        if part not in mod._modules:
+            mod.add_module(part, nn.Module())
+        mod = mod._modules[part]
+    return mod
+
+
+class VapGPT(nn.Module):
+    """vap/model.py:125-268 on the MI355X engine."""
+
+    def __init__(self, conf: Optional[VapConfig] = None, precision: Optional[str] = None, lstm_layers: int = 1):
+        super().__init__()
+        if conf is None:
+            conf = VapConfig()
+        self.conf = conf
+        self.sample_rate = conf.sample_rate
+        self.frame_hz = conf.frame_hz
+        self.precision = precision or os.environ.get("VAP_PRECISION", "fp32")
+        if self.precision not in N.PRECISION:
+            raise ValueError(f"precision must be one of {list(N.PRECISION)}")
+        self.lstm_layers = lstm_layers
+        self.objective = ObjectiveVAP(bin_times=conf.bin_times, frame_hz=conf.frame_hz)
+        self._build_params(lstm_layers)
+        self._handle = None
+        self._handle_key = None
+        self._dirty = True
+        self._ws: Optional[Tensor] = None
+
+    # ------------------------------------------------------------------ parameters / state dict
+    def _schema(self, lstm_layers: int):
+        c = self.conf
+        return _schema(dim=c.dim, channel_layers=c.channel_layers, cross_layers=c.cross_layers,
+                       num_heads=c.num_heads, lstm_layers=lstm_layers, n_bins=len(c.bin_times))
+
+    def _build_params(self, lstm_layers: int):
+        c = self.conf
+        init = synthetic_state_dict(seed=0, dim=c.dim, channel_layers=c.channel_layers,
+                                    cross_layers=c.cross_layers, num_heads=c.num_heads,
+                                    lstm_layers=lstm_layers, n_bins=len(c.bin_times))
+        for key, shape in self._schema(lstm_layers):
+            if key == "objective.codebook.emb.weight":
+                continue  # owned by ObjectiveVAP.codebook.emb
+            prefix, name = key.rsplit(".", 1)
+            mod = _container(self, prefix)
+            mod.register_parameter(name, nn.Parameter(torch.from_numpy(init[key]).reshape(shape),
+                                                      requires_grad=False))
+        self.lstm_layers = lstm_layers
+
+    def _drop_lstm(self):
+        base = self.encoder.encoder.gAR.baseNet
+        for name in list(base._parameters):
+            del base._parameters[name]
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """nn.Module.load_state_dict with the LSTM depth inferred from the keys."""
+        n = 0
+        while f"encoder.encoder.gAR.baseNet.weight_ih_l{n}" in state_dict:
+            n += 1
+        if n and n != self.lstm_layers:
+            dev = next(self.parameters()).device
+            self._drop_lstm()
+            self.lstm_layers = n
+            p = "encoder.encoder.gAR.baseNet"
+            base = self.encoder.encoder.gAR.baseNet
+            for key, shape in self._schema(n):
+                if key.startswith(p + "."):
+                    base.register_parameter(key[len(p) + 1:], nn.Parameter(torch.zeros(shape, device=dev),
+                                                                          requires_grad=False))
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._dirty = True
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        self._dirty = True
+        self._ws = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def invalidate(self):
+        """Call after modifying parameters in place (re-packs the kernel layouts on next use)."""
+        self._dirty = True
+
+    def set_precision(self, precision: str):
+        if precision not in N.PRECISION:
+            raise ValueError(f"precision must be one of {list(N.PRECISION)}")
+        self.precision = precision
+        self._dirty = True
+        self._ws = None
+
+    # ------------------------------------------------------------------ native handle
+    def _free_handle(self):
+        if self._handle is not None:
+            try:
+                N.lib().vap_destroy(self._handle)
+            except Exception:
+                pass
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self._free_handle()
+        except Exception:
+            pass
+
+    def _native(self, device: torch.device):
+        key = (device, self.precision, self.lstm_layers)
+        if self._handle is not None and not self._dirty and self._handle_key == key:
+            return self._handle
+        lib = N.lib()
+        self._free_handle()
+        c = self.conf
+        dims = N.VapDims(c.dim, c.num_heads, c.channel_layers, c.cross_layers, self.lstm_layers,
+                         len(c.bin_times), N.PRECISION[self.precision])
+        h = ctypes.c_void_p()
+        N.check(lib.vap_create(ctypes.byref(dims), ctypes.byref(h)), "vap_create")
+        self._handle = h
+        sd = self.state_dict()
+        st = N.stream_ptr(device)
+        keep = []
+        n = ctypes.c_int()
+        N.check(lib.vap_num_params(h, ctypes.byref(n)))
+        for i in range(n.value):
+            k = ctypes.c_char_p()
+            numel = ctypes.c_int64()
+            N.check(lib.vap_param_info(h, i, ctypes.byref(k), ctypes.byref(numel)))
+            name = k.value.decode()
+            if name not in sd:
+                raise RuntimeError(f"Missing key in state_dict: {name}")
+            t = sd[name]
+            if t.device != device:
+                raise RuntimeError(f"Expected all tensors to be on the same device, but found {t.device} "
+                                   f"(parameter {name}) and {device} (input); call model.to({str(device)!r})")
+            t = t.detach().float().contiguous()
+            keep.append(t)
+            N.check(lib.vap_set_param(h, name.encode(), t.data_ptr(), t.numel(), st), "vap_set_param")
+        N.check(lib.vap_finalize(h, st), "vap_finalize")
+        del keep
+        self._handle_key = key
+        self._dirty = False
+        return h
+
+    def _workspace(self, h, B: int, n: int, device) -> Tensor:
+        need = ctypes.c_size_t()
+        N.check(N.lib().vap_workspace_size(h, B, n, ctypes.byref(need)), "vap_workspace_size")
+        if self._ws is None or self._ws.numel() < need.value or self._ws.device != device:
+            self._ws = None
+            self._ws = torch.empty(need.value, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def _check_input(self, waveform: Tensor) -> Tensor:
+        assert waveform.shape[1] == 2, f"audio VAP ENCODER: {waveform.shape} != (B, 2, n_samples)"
+        if not waveform.is_cuda:
+            raise RuntimeError("VapGPT (MI355X engine) runs on HIP devices only: move the model and the waveform "
+                               "to 'cuda' (there is no CPU fallback)")
+        return waveform.float().contiguous()
+
+    # ------------------------------------------------------------------ reference API
+    @property
+    def horizon_time(self):
+        return self.objective.horizon_time
+
+    def encode_audio(self, audio: Tensor) -> Tuple[Tensor, Tensor]:
+        """vap/model.py:169-175: EncoderCPC on each speaker -> (x1, x2), each (B, T, 256)."""
+        audio = self._check_input(audio)
+        B, _, n = audio.shape
+        T = N.frame_lengths(n)[-1]
+        h = self._native(audio.device)
+        ws = self._workspace(h, B, n, audio.device)
+        out = torch.empty(2, B, T, self.conf.dim, device=audio.device, dtype=torch.float32)
+        N.check(N.lib().vap_encode(h, audio.data_ptr(), B, n, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   N.stream_ptr(audio.device)), "vap_encode")
+        return out[0], out[1]
+
+    def forward(self, waveform: Tensor, attention: bool = False) -> Dict[str, Tensor]:
+        """vap/model.py:249-268 -> {"logits": (B, T, 256), "vad": (B, T, 2)}."""
+        if attention:
+            raise NotImplementedError("attention maps (attention=True) are not produced by the MI355X engine "
+                                      "(SURVEY.md §8(f) rank 4)")
+        waveform = self._check_input(waveform)
+        B, _, n = waveform.shape
+        T = N.frame_lengths(n)[-1]
+        if T <= 0:
+            raise RuntimeError(f"waveform of {n} samples is too short for one frame")
+        h = self._native(waveform.device)
+        ws = self._workspace(h, B, n, waveform.device)
+        logits = torch.empty(B, T, self.objective.n_classes, device=waveform.device, dtype=torch.float32)
+        vad = torch.empty(B, T, 2, device=waveform.device, dtype=torch.float32)
+        N.check(N.lib().vap_forward(h, waveform.data_ptr(), B, n, logits.data_ptr(), vad.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), N.stream_ptr(waveform.device)), "vap_forward")
+        return {"logits": logits, "vad": vad}
+
+    @torch.no_grad()
+    def probs(self, waveform: Tensor, vad: Optional[Tensor] = None, now_lims: List[int] = [0, 1],
+              future_lims: List[int] = [2, 3]) -> Dict[str, Tensor]:
+        """vap/model.py:180-225, including quirk Q1: labels always come from the model's own sigmoid
+        VAD (the ``vad`` argument is shadowed), so ``loss`` is always returned."""
+        out = self(waveform)
+        logits, vad_logits = out["logits"], out["vad"]
+        B, T, C = logits.shape
+        dev = logits.device
+        probs = torch.empty_like(logits)
+        vad = torch.empty(B, T, 2, device=dev)
+        p_now = torch.empty(B, T, 2, device=dev)
+        p_future = torch.empty(B, T, 2, device=dev)
+        H = torch.empty(B, T, device=dev)
+        st = N.stream_ptr(dev)
+        N.check(N.lib().vap_probs(logits.data_ptr(), vad_logits.data_ptr(), B, T, self.objective.n_bins,
+                                  now_lims[0], now_lims[-1], future_lims[0], future_lims[1], probs.data_ptr(),
+                                  vad.data_ptr(), p_now.data_ptr(), p_future.data_ptr(), H.data_ptr(), st),
+                "vap_probs")
+        ret = {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H}
+        _, loss = self.objective.labels_and_loss(vad, logits)
+        ret["loss"] = loss
+        return ret
+
+    @torch.no_grad()
+    def vad(self, waveform: Tensor, max_fill_silence_time: float = 0.02, max_omit_spike_time: float = 0.02,
+            vad_cutoff: float = 0.5) -> Tensor:
+        """vap/model.py:227-247: binary VAD with short silences filled and short spikes removed."""
+        vl = self(waveform)["vad"]
+        B, T, _ = vl.shape
+        out = torch.empty_like(vl)
+        N.check(N.lib().vap_vad_postprocess(vl.data_ptr(), B, T, float(vad_cutoff),
+                                            round(max_fill_silence_time * self.frame_hz),
+                                            round(max_omit_spike_time * self.frame_hz), out.data_ptr(),
+                                            N.stream_ptr(vl.device)), "vap_vad_postprocess")
+        return out
+
+
+class VAPModel(VapGPT):
+    """Inference alias for the reference's ``vap.train.VAPModel`` (vap/train.py:244): a VapGPT."""
+
+    def __init__(self, conf: Optional[VapConfig] = None, *args, **kwargs):
+        super().__init__(conf, *args, **kwargs)
