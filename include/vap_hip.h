@@ -122,8 +122,8 @@ int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, cons
 int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq, const void* K, int64_t k_ld,
                        int64_t k_seq, const void* V, int64_t v_ld, int64_t v_seq, void* O, int64_t o_ld,
                        int64_t o_seq, const float* slopes, int S, int T, int H, int kv_swap, float scale, void* stream);
-int vap_test_lstm(int precision, const float* gx, int S, int T, const float* whh, void* whh_packed, void* out,
-                  void* stream);
+int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh, void* whh_packed, void* out,
+                  int variant, void* stream);
 int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
                    const float* gamma, const float* beta, void* out, void* stream);
 int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,

@@ -125,18 +125,23 @@ def test_attention(prec, kv_swap):
     assert err <= tol, f"{prec}: attention max err {err}"
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_lstm(prec):
+@pytest.mark.parametrize("prec,variant", [("fp32", 0), ("bf16", 0), ("bf16", 1)])
+def test_lstm(prec, variant):
+    """variant 0 = the engine's kernel for that precision (bf16: W_hh resident in AGPR/VGPR/LDS,
+    bf16 gx); variant 1 = the L2-streaming kernel in bf16 (fp32 gx)."""
     N = lib()
     code, dt = PREC[prec]
     g = torch.Generator().manual_seed(3)
     S, T = 20, 37
     gx = torch.randn(S, T, 1024, generator=g)
+    if prec == "bf16" and variant == 0:
+        gx = gx.to(torch.bfloat16).float()
     whh = (torch.rand(1024, 256, generator=g) * 2 - 1) / 16
     out = torch.zeros(S, T, 256, device="cuda", dtype=dt)
     packed = torch.zeros(1024 * 256, device="cuda", dtype=dt)
-    gxd, whd = gx.cuda(), whh.cuda()
-    _run(N.lib().vap_test_lstm, code, _p(gxd), S, T, _p(whd), _p(packed), _p(out), _st())
+    gxd = gx.cuda().to(torch.bfloat16) if (prec == "bf16" and variant == 0) else gx.cuda()
+    whd = whh.cuda()
+    _run(N.lib().vap_test_lstm, code, _p(gxd), S, T, _p(whd), _p(packed), _p(out), variant, _st())
     wr = whh.to(dt).float()
     h = torch.zeros(S, 256)
     c = torch.zeros(S, 256)

@@ -181,3 +181,19 @@ def test_batch_20s_bf16(m16, golden):
     out = m16.probs(torch.from_numpy(w).cuda())
     errs = _cmp(out, g, BF16_TOL)
     print("bf16 20 s max abs err:", errs)
+
+
+def test_bf16_multi_workgroup_batch_invariance(m16, m32):
+    """B = 9 -> 18 sequences -> two LSTM workgroups (16 sequences each) in bf16 mode: every clip's
+    outputs must be bit-identical to running that clip alone, and close to fp32 parity mode."""
+    n = 40960
+    w = torch.from_numpy(np.stack([synthetic_waveform(200 + i, n) for i in range(9)])).cuda()
+    full = m16.probs(w)
+    ref = m32.probs(w)
+    for i in (0, 8):
+        one = m16.probs(w[i:i + 1])
+        for k in full:
+            assert torch.equal(full[k][i:i + 1], one[k]), f"bf16 batch dependence in {k} (clip {i})"
+    for k in ("p_now", "p_future", "vad"):
+        err = (full[k] - ref[k]).abs().max().item()
+        assert err <= BF16_TOL[k], (k, err)

@@ -104,6 +104,175 @@ __global__ void pack_whh_kernel(const float* __restrict__ whh, T* __restrict__ o
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16 perf mode: W_hh RESIDENT on the CU.  512 KiB bf16 = 4 waves (one per SIMD, 512-register
+// budget each) x 128 fragments of 1 KiB: 90 per wave in registers, 38 per wave in LDS (152 KiB),
+// so a step reads no weights from L2/HBM.  Wave w owns units [64w, 64w+64): row tiles
+// rt = g*4 + ut (rows g*256 + 64w + 16ut + lane&15), k-groups kg (k = 32kg + 8(lane>>4) + e),
+// fragment f = rt*8 + kg.  h_{t-1} lives in an 8 KiB LDS image [seq][256] with chunk ^= seq
+// (conflict-free b128 reads).  gx (bf16) of step t+1 is prefetched while step t computes.
+// ------------------------------------------------------------------------------------------
+constexpr int R_NW = 4, R_NF = 128, R_NAGPR = 64, R_NVGPR = 26, R_NREG = R_NAGPR + R_NVGPR, R_NLDS = R_NF - R_NREG;
+
+VAP_DEV float fsig(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+VAP_DEV float ftanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
+
+// MFMA with the A operand in AGPRs / VGPRs, issued as inline asm so the compiler keeps the
+// weight fragments resident in the accumulator file instead of spilling/copying them per use.
+// hipcc pads no hazards inside asm: LEAD adds the VALU-write -> MFMA-srcC wait (s_nop 1); TAIL
+// adds the MFMA-D -> VALU-read wait (16 states) after the last MFMA of a block.
+// The waits live INSIDE the MFMA's asm string: a separate "s_nop" statement has no operands, so
+// the compiler may legally schedule the VALU consumer of the MFMA output ahead of it (observed:
+// stale accumulators on some lanes).
+#define VAP_MFMA_ASM(LEAD, TAIL, ACON)                                                              \
+  do {                                                                                             \
+    if constexpr (LEAD && TAIL)                                                                    \
+      asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 15"                 \
+                   : "+v"(c) : ACON(a), "v"(b));                                                    \
+    else if constexpr (LEAD)                                                                       \
+      asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : ACON(a), "v"(b)); \
+    else if constexpr (TAIL)                                                                       \
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 15" : "+v"(c) : ACON(a), "v"(b)); \
+    else                                                                                           \
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : ACON(a), "v"(b));         \
+  } while (0)
+
+template <int LEAD, int TAIL>
+VAP_DEV void mfma_a(f32x4& c, const chunk16& a, const chunk16& b) {
+  VAP_MFMA_ASM(LEAD, TAIL, "a");
+}
+template <int LEAD, int TAIL>
+VAP_DEV void mfma_v(f32x4& c, const chunk16& a, const chunk16& b) {
+  VAP_MFMA_ASM(LEAD, TAIL, "v");
+}
+
+template <int F, int LEAD, int TAIL>
+VAP_DEV void mfma_frag(f32x4& c, const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR], const chunk16* wl,
+                       const chunk16& hf) {
+  if constexpr (F < R_NAGPR) {
+    mfma_a<LEAD, TAIL>(c, wa[F], hf);
+  } else if constexpr (F < R_NREG) {
+    mfma_v<LEAD, TAIL>(c, wv[F - R_NAGPR], hf);
+  } else {
+    const chunk16 a = wl[(F - R_NREG) * 64];
+    mfma_v<LEAD, TAIL>(c, a, hf);
+  }
+}
+
+template <int UT, int KG>
+VAP_DEV void lstm_kstep(f32x4 (&acc)[4], const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR],
+                        const chunk16* wl, const unsigned char* hb, int sl, int lane) {
+  const chunk16 hf = *(const chunk16*)(hb + sl * 512 + (((KG * 4 + (lane >> 4)) ^ sl) << 4));
+  constexpr int LEAD = KG == 0 ? 1 : 0;
+  // TAIL on every MFMA of the last k-step: the compiler may place the VALU reading acc[g] right
+  // after acc[g]'s asm statement.
+  constexpr int TAIL = KG == 7 ? 1 : 0;
+  mfma_frag<(0 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[0], wa, wv, wl, hf);
+  mfma_frag<(1 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[1], wa, wv, wl, hf);
+  mfma_frag<(2 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[2], wa, wv, wl, hf);
+  mfma_frag<(3 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[3], wa, wv, wl, hf);
+}
+
+template <int UT>
+VAP_DEV void lstm_unit_tile(f32x4 (&acc)[4], const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR],
+                            const chunk16* wl, const unsigned char* hb, int sl, int lane) {
+  lstm_kstep<UT, 0>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 1>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 2>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 3>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 4>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 5>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 6>(acc, wa, wv, wl, hb, sl, lane);
+  lstm_kstep<UT, 7>(acc, wa, wv, wl, hb, sl, lane);
+}
+
+template <int UT>
+VAP_DEV void lstm_tile_step(bf16x4 (&gn)[4][4], float (&c)[4][4], float (&hv)[4][4], const bf16* gt,
+                            const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR], const chunk16* wl,
+                            const unsigned char* hb, int sl, int lane) {
+  f32x4 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    acc[g] = f32x4{(float)gn[UT][g][0], (float)gn[UT][g][1], (float)gn[UT][g][2], (float)gn[UT][g][3]};
+    gn[UT][g] = *(const bf16x4*)(gt + g * HD + UT * 16);  // prefetch step t+1
+  }
+  lstm_unit_tile<UT>(acc, wa, wv, wl, hb, sl, lane);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float ig = fsig(acc[0][r]), fg = fsig(acc[1][r]), gg = ftanh(acc[2][r]), og = fsig(acc[3][r]);
+    c[UT][r] = fg * c[UT][r] + ig * gg;
+    hv[UT][r] = og * ftanh(c[UT][r]);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __restrict__ gx, int S, int Tn,
+                                                              const chunk16* __restrict__ wp, bf16* __restrict__ out,
+                                                              int64_t out_seq_stride) {
+  __shared__ __attribute__((aligned(16))) chunk16 wls[R_NW * R_NLDS * 64];
+  __shared__ __attribute__((aligned(16))) unsigned char hb[NS * 512];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int sl = lane & 15;  // sequence within the group (MFMA column)
+  const int seq = blockIdx.x * NS + sl;
+  const bool valid = seq < S;
+
+  chunk16 wa[R_NAGPR], wv[R_NVGPR];
+  const chunk16* wsrc = wp + (int64_t)w * R_NF * 64 + lane;
+#pragma unroll
+  for (int f = 0; f < R_NAGPR; ++f) wa[f] = wsrc[f * 64];
+#pragma unroll
+  for (int f = 0; f < R_NVGPR; ++f) wv[f] = wsrc[(R_NAGPR + f) * 64];
+  chunk16* wl = wls + w * R_NLDS * 64 + lane;
+#pragma unroll
+  for (int f = 0; f < R_NLDS; ++f) wl[f * 64] = wsrc[(R_NREG + f) * 64];
+  for (int i = tid; i < NS * 512 / 4; i += 256) ((unsigned*)hb)[i] = 0u;
+  float c[4][4];
+#pragma unroll
+  for (int ut = 0; ut < 4; ++ut)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[ut][r] = 0.f;
+
+  const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + 64 * w + (lane >> 4) * 4;
+  bf16x4 gn[4][4];
+#pragma unroll
+  for (int ut = 0; ut < 4; ++ut)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gn[ut][g] = *(const bf16x4*)(gxs + g * HD + ut * 16);
+  __syncthreads();
+
+  for (int t = 0; t < Tn; ++t) {
+    const bf16* gt = gxs + (int64_t)(t + 1 < Tn ? t + 1 : t) * G4;
+    float hv[4][4];
+    lstm_tile_step<0>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
+    lstm_tile_step<1>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
+    lstm_tile_step<2>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
+    lstm_tile_step<3>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
+    __syncthreads();  // every wave has consumed h_{t-1}
+#pragma unroll
+    for (int ut = 0; ut < 4; ++ut) {
+      const int u = 64 * w + 16 * ut + (lane >> 4) * 4;
+      bf16x4 hv4 = {(bf16)hv[ut][0], (bf16)hv[ut][1], (bf16)hv[ut][2], (bf16)hv[ut][3]};
+      *(bf16x4*)(hb + sl * 512 + (((u >> 3) ^ sl) << 4) + (u & 7) * 2) = hv4;
+      if (valid) *(bf16x4*)(out + (int64_t)seq * out_seq_stride + (int64_t)t * HD + u) = hv4;
+    }
+    __syncthreads();  // h_t visible to every wave
+  }
+}
+
+// Wp[w][f = rt*8 + kg][lane][e] = W[g*256 + 64w + 16ut + (l&15)][32kg + 8(l>>4) + e],  rt = g*4 + ut
+__global__ void pack_whh_resident_kernel(const float* __restrict__ whh, bf16* __restrict__ out) {
+  const int64_t n = (int64_t)G4 * HD;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7);
+    const int l = (int)((i >> 3) & 63);
+    const int f = (int)((i >> 9) & 127);
+    const int w = (int)(i >> 16);
+    const int rt = f >> 3, kg = f & 7, g = rt >> 2, ut = rt & 3;
+    const int row = g * HD + 64 * w + 16 * ut + (l & 15);
+    const int k = 32 * kg + 8 * (l >> 4) + e;
+    out[i] = (bf16)whh[(int64_t)row * HD + k];
+  }
+}
+
 }  // namespace
 
 template <typename T>
@@ -118,6 +287,18 @@ hipError_t launch_lstm(const float* gx, int S, int Tn, const T* whh_packed, T* o
 template <typename T>
 hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st) {
   hipLaunchKernelGGL((pack_whh_kernel<T>), dim3(256), dim3(256), 0, st, whh, packed);
+  return hipGetLastError();
+}
+
+hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
+                                int64_t out_seq_stride, hipStream_t st) {
+  if (S <= 0 || Tn <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lstm_resident_kernel, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
+                     (const chunk16*)whh_packed, out, out_seq_stride);
+  return hipGetLastError();
+}
+hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st) {
+  hipLaunchKernelGGL(pack_whh_resident_kernel, dim3(256), dim3(256), 0, st, whh, packed);
   return hipGetLastError();
 }
 

@@ -260,7 +260,10 @@ int pack_all(vap_handle* h, hipStream_t st) {
     if (!wih || !whh || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
     h->fpacked["bias" + s] = b;
     HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
-    HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
+    if constexpr (sizeof(T) == 2)
+      HIPCHK(launch_pack_whh_resident(h->P(p + "weight_hh" + s), whh, st));
+    else
+      HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
     HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
   }
   {
@@ -450,14 +453,20 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
     const std::string s = "_l" + std::to_string(l);
     const T* in = l == 0 ? X4 + D : Hb[(l - 1) & 1] + 4 * D;
     const int64_t in_seq = l == 0 ? p.s4 : p.sh;
+    // bf16 mode: gx stored bf16 and the recurrence runs with W_hh resident on the CU
+    constexpr bool bf = sizeof(T) == 2;
     {
       Timed tm(h, VAP_K_LSTM_PROJ, st);
       HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L[4], S, GX,
-                           4 * D, L[4] * 4 * D), st, true));
+                           4 * D, L[4] * 4 * D), st, !bf));
     }
     {
       Timed tm(h, VAP_K_LSTM_REC, st);
-      HIPCHK(launch_lstm<T>(GX, S, (int)L[4], h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, st));
+      if constexpr (bf)
+        HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L[4], (const bf16*)h->W<T>("whh" + s),
+                                    (bf16*)(Hb[l & 1] + 4 * D), p.sh, st));
+      else
+        HIPCHK(launch_lstm<T>(GX, S, (int)L[4], h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, st));
     }
   }
   {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)

@@ -46,6 +46,10 @@ hipError_t launch_lstm(const float* gx, int S, int Tn, const T* whh_packed, T* o
                        hipStream_t st);
 template <typename T>
 hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st);
+// bf16 perf mode: W_hh resident in VGPRs + LDS (8 waves / CU), gx in bf16 [S][T][1024]
+hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
+                                int64_t out_seq_stride, hipStream_t st);
+hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st);
 
 struct AttnArgs {
   const void* Q; int64_t q_ld, q_seq;     // head h at column h*64

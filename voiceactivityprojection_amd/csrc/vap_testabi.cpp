@@ -69,18 +69,25 @@ int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq
   return rc_of(precision == VAP_PRECISION_BF16 ? launch_attention<bf16>(a, st) : launch_attention<float>(a, st));
 }
 
-// whh_packed: scratch of 1024*256 storage elements; out: [S][T][256] storage type
-int vap_test_lstm(int precision, const float* gx, int S, int T, const float* whh, void* whh_packed, void* out,
-                  void* stream) {
+// gx: [S][T][1024] storage type for bf16 (the engine's resident kernel) / fp32 for fp32;
+// variant 1 = the L2-streaming bf16 kernel (fp32 gx).  whh_packed: scratch of 1024*256 storage
+// elements; out: [S][T][256] storage type.
+int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh, void* whh_packed, void* out,
+                  int variant, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (precision == VAP_PRECISION_BF16 && variant == 0) {
+    hipError_t e = launch_pack_whh_resident(whh, (bf16*)whh_packed, st);
+    if (e != hipSuccess) return VAP_ERR_HIP;
+    return rc_of(launch_lstm_resident((const bf16*)gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st));
+  }
   if (precision == VAP_PRECISION_BF16) {
     hipError_t e = launch_pack_whh<bf16>(whh, (bf16*)whh_packed, st);
     if (e != hipSuccess) return VAP_ERR_HIP;
-    return rc_of(launch_lstm<bf16>(gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st));
+    return rc_of(launch_lstm<bf16>((const float*)gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st));
   }
   hipError_t e = launch_pack_whh<float>(whh, (float*)whh_packed, st);
   if (e != hipSuccess) return VAP_ERR_HIP;
-  return rc_of(launch_lstm<float>(gx, S, T, (const float*)whh_packed, (float*)out, (int64_t)T * 256, st));
+  return rc_of(launch_lstm<float>((const float*)gx, S, T, (const float*)whh_packed, (float*)out, (int64_t)T * 256, st));
 }
 
 // out: [2B][L0 + 4][256] storage type (pad rows untouched)
