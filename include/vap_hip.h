@@ -126,6 +126,8 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
                   int variant, void* stream);
 int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
                    const float* gamma, const float* beta, void* out, void* stream);
+/* one v_mfma_f32_16x16x4_f32 with lane-provided operands a[64], b[64] -> d[64][4] (layout probe) */
+int vap_test_probe_mfma_f32(const float* a, const float* b, float* d, void* stream);
 int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
                        void* raw, void* stream);
 

@@ -14,7 +14,7 @@
 Extra (engine) knobs: ``precision`` ("fp32" parity mode, default; "bf16" perf mode) as a
 constructor argument / ``VAP_PRECISION`` env var, and ``lstm_layers`` (inferred from state dicts).
 """
-from __future__ import annotations
+
 
 import ctypes
 import os
