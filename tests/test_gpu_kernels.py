@@ -96,7 +96,7 @@ def test_gemm(prec, case):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("kv_swap", [0, 2])
+@pytest.mark.parametrize("kv_swap", [0, 1])
 def test_attention(prec, kv_swap):
     N = lib()
     code, dt = PREC[prec]
@@ -111,7 +111,7 @@ def test_attention(prec, kv_swap):
     Qd, Kd, Vd, sd = Q.cuda(), K.cuda(), V.cuda(), slopes.cuda()
     _run(N.lib().vap_test_attention, code, _p(Qd), D, T * D, _p(Kd), D, T * D, _p(Vd), D, T * D, _p(O), D, T * D,
          _p(sd), S, T, H, kv_swap, scale, _st())
-    kv = [(s + kv_swap) % S for s in range(S)]
+    kv = [(s ^ 1) if kv_swap else s for s in range(S)]  # cross: other speaker of the clip
     q = Q.float().view(S, T, H, 64).transpose(1, 2)
     k = K.float()[kv].view(S, T, H, 64).transpose(1, 2)
     v = V.float()[kv].view(S, T, H, 64).transpose(1, 2)
@@ -173,7 +173,7 @@ def test_conv0(prec):
     out = torch.zeros(2 * B, L0 + 4, 256, device="cuda", dtype=dt)
     d = [t.cuda() for t in (wav, w0, b0, ga, be)]
     _run(N.lib().vap_test_conv0, code, _p(d[0]), B, n, L0, _p(d[1]), _p(d[2]), _p(d[3]), _p(d[4]), _p(out), _st())
-    x = torch.cat([wav[:, 0:1], wav[:, 1:2]], 0)  # channel-major sequences
+    x = wav.reshape(2 * B, 1, n)  # clip-major sequences (seq = 2*clip + channel)
     y = F.conv1d(x, w0, b0, stride=5, padding=3)
     mu, var = y.mean(1, keepdim=True), y.var(1, keepdim=True)
     y = torch.relu((y - mu) * torch.rsqrt(var + 1e-5) * ga.view(1, -1, 1) + be.view(1, -1, 1)).transpose(1, 2)

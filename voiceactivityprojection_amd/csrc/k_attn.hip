@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
-  const int ks = (s + a.kv_swap) % a.S;
+  const int ks = a.kv_swap ? (s ^ 1) : s;  // cross-attention: the other speaker of the same clip
   const T* Qs = (const T*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
   const T* Ks = (const T*)a.K + (int64_t)ks * a.k_seq + h * HDIM;
   const T* Vs = (const T*)a.V + (int64_t)ks * a.v_seq + h * HDIM;

@@ -146,63 +146,88 @@ VAP_DEV void mfma_v(f32x4& c, const chunk16& a, const chunk16& b) {
   VAP_MFMA_ASM(LEAD, TAIL, "v");
 }
 
+// One cell of the LSTM update for register r of a finished unit tile.
+VAP_DEV void lstm_cell(const f32x4 (&acc)[4], int r, float& c, float& h) {
+  const float ig = fsig(acc[0][r]), fg = fsig(acc[1][r]), gg = ftanh(acc[2][r]), og = fsig(acc[3][r]);
+  c = fg * c + ig * gg;
+  h = og * ftanh(c);
+}
+
+// LDS operands of one k-step q = ut*8 + kg: the h fragment and the LDS-resident weight fragments
+// (gate 3 always, gate 2 for the last ones).  Gates 0/1 live in AGPRs, gate 2 mostly in VGPRs.
+struct KPre {
+  chunk16 hf, w2, w3;
+};
+
+template <int Q>
+VAP_DEV void kload(KPre& p, const chunk16* wl, const unsigned char* hb, int sl, int lane) {
+  constexpr int UT = Q >> 3, KG = Q & 7;
+  constexpr int F2 = (2 * 4 + UT) * 8 + KG, F3 = (3 * 4 + UT) * 8 + KG;
+  p.hf = *(const chunk16*)(hb + sl * 512 + (((KG * 4 + (lane >> 4)) ^ sl) << 4));
+  if constexpr (F2 >= R_NREG) p.w2 = wl[(F2 - R_NREG) * 64];
+  if constexpr (F3 >= R_NREG) p.w3 = wl[(F3 - R_NREG) * 64];
+}
+
 template <int F, int LEAD, int TAIL>
-VAP_DEV void mfma_frag(f32x4& c, const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR], const chunk16* wl,
-                       const chunk16& hf) {
-  if constexpr (F < R_NAGPR) {
+VAP_DEV void mfma_f(f32x4& c, const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR], const chunk16& lds,
+                    const chunk16& hf) {
+  if constexpr (F < R_NAGPR)
     mfma_a<LEAD, TAIL>(c, wa[F], hf);
-  } else if constexpr (F < R_NREG) {
+  else if constexpr (F < R_NREG)
     mfma_v<LEAD, TAIL>(c, wv[F - R_NAGPR], hf);
-  } else {
-    const chunk16 a = wl[(F - R_NREG) * 64];
-    mfma_v<LEAD, TAIL>(c, a, hf);
-  }
+  else
+    mfma_v<LEAD, TAIL>(c, lds, hf);
 }
 
-template <int UT, int KG>
-VAP_DEV void lstm_kstep(f32x4 (&acc)[4], const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR],
-                        const chunk16* wl, const unsigned char* hb, int sl, int lane) {
-  const chunk16 hf = *(const chunk16*)(hb + sl * 512 + (((KG * 4 + (lane >> 4)) ^ sl) << 4));
+struct LstmState {
+  bf16x4 gn[4][4];  // gx of the next step (prefetched)
+  float c[4][4];    // cell state: unit 64w + 16ut + 4(lane>>4) + r, sequence lane&15
+  float hv[4][4];   // h_t of this step
+  f32x4 acc[4], prev[4];
+};
+
+// k-step Q of the step: issue the LDS reads of step Q+1, then the four MFMAs of step Q; the cell
+// update of the previous unit tile is interleaved (one register per two k-steps) so the vector
+// and matrix pipes of the SIMD overlap.
+template <int Q>
+VAP_DEV void kstep(LstmState& st, const KPre& cur, KPre& nxt, const bf16* gt, const chunk16 (&wa)[R_NAGPR],
+                   const chunk16 (&wv)[R_NVGPR], const chunk16* wl, const unsigned char* hb, int sl, int lane) {
+  constexpr int UT = Q >> 3, KG = Q & 7;
+  if constexpr (KG == 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      st.acc[g] = f32x4{(float)st.gn[UT][g][0], (float)st.gn[UT][g][1], (float)st.gn[UT][g][2],
+                        (float)st.gn[UT][g][3]};
+      st.gn[UT][g] = *(const bf16x4*)(gt + g * HD + UT * 16);  // prefetch step t+1
+    }
+  }
+  if constexpr (Q + 1 < 32) kload<Q + 1>(nxt, wl, hb, sl, lane);
   constexpr int LEAD = KG == 0 ? 1 : 0;
-  // TAIL on every MFMA of the last k-step: the compiler may place the VALU reading acc[g] right
-  // after acc[g]'s asm statement.
-  constexpr int TAIL = KG == 7 ? 1 : 0;
-  mfma_frag<(0 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[0], wa, wv, wl, hf);
-  mfma_frag<(1 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[1], wa, wv, wl, hf);
-  mfma_frag<(2 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[2], wa, wv, wl, hf);
-  mfma_frag<(3 * 4 + UT) * 8 + KG, LEAD, TAIL>(acc[3], wa, wv, wl, hf);
+  constexpr int TAIL = (UT == 3 && KG == 7) ? 1 : 0;  // only the last tile's results are read right away
+  mfma_f<(0 * 4 + UT) * 8 + KG, LEAD, TAIL>(st.acc[0], wa, wv, cur.w2, cur.hf);
+  mfma_f<(1 * 4 + UT) * 8 + KG, LEAD, TAIL>(st.acc[1], wa, wv, cur.w2, cur.hf);
+  mfma_f<(2 * 4 + UT) * 8 + KG, LEAD, TAIL>(st.acc[2], wa, wv, cur.w2, cur.hf);
+  mfma_f<(3 * 4 + UT) * 8 + KG, LEAD, TAIL>(st.acc[3], wa, wv, cur.w3, cur.hf);
+  if constexpr (UT > 0) {
+    if constexpr (KG == 1)  // consumers of the previous tile stay below this point (no MFMA->VALU hazard)
+      asm volatile("" : "+v"(st.prev[0]), "+v"(st.prev[1]), "+v"(st.prev[2]), "+v"(st.prev[3]));
+    if constexpr (KG & 1) lstm_cell(st.prev, KG >> 1, st.c[UT - 1][KG >> 1], st.hv[UT - 1][KG >> 1]);
+  }
+  if constexpr (KG == 7) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) st.prev[g] = st.acc[g];
+    if constexpr (UT == 3) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lstm_cell(st.prev, r, st.c[3][r], st.hv[3][r]);
+    }
+  }
 }
 
-template <int UT>
-VAP_DEV void lstm_unit_tile(f32x4 (&acc)[4], const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR],
-                            const chunk16* wl, const unsigned char* hb, int sl, int lane) {
-  lstm_kstep<UT, 0>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 1>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 2>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 3>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 4>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 5>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 6>(acc, wa, wv, wl, hb, sl, lane);
-  lstm_kstep<UT, 7>(acc, wa, wv, wl, hb, sl, lane);
-}
-
-template <int UT>
-VAP_DEV void lstm_tile_step(bf16x4 (&gn)[4][4], float (&c)[4][4], float (&hv)[4][4], const bf16* gt,
-                            const chunk16 (&wa)[R_NAGPR], const chunk16 (&wv)[R_NVGPR], const chunk16* wl,
-                            const unsigned char* hb, int sl, int lane) {
-  f32x4 acc[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    acc[g] = f32x4{(float)gn[UT][g][0], (float)gn[UT][g][1], (float)gn[UT][g][2], (float)gn[UT][g][3]};
-    gn[UT][g] = *(const bf16x4*)(gt + g * HD + UT * 16);  // prefetch step t+1
-  }
-  lstm_unit_tile<UT>(acc, wa, wv, wl, hb, sl, lane);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float ig = fsig(acc[0][r]), fg = fsig(acc[1][r]), gg = ftanh(acc[2][r]), og = fsig(acc[3][r]);
-    c[UT][r] = fg * c[UT][r] + ig * gg;
-    hv[UT][r] = og * ftanh(c[UT][r]);
-  }
+template <int Q>
+VAP_DEV void ksteps(LstmState& st, KPre& cur, KPre& nxt, const bf16* gt, const chunk16 (&wa)[R_NAGPR],
+                    const chunk16 (&wv)[R_NVGPR], const chunk16* wl, const unsigned char* hb, int sl, int lane) {
+  kstep<Q>(st, cur, nxt, gt, wa, wv, wl, hb, sl, lane);
+  if constexpr (Q + 1 < 32) ksteps<Q + 1>(st, nxt, cur, gt, wa, wv, wl, hb, sl, lane);
 }
 
 __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __restrict__ gx, int S, int Tn,
@@ -225,36 +250,35 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
 #pragma unroll
   for (int f = 0; f < R_NLDS; ++f) wl[f * 64] = wsrc[(R_NREG + f) * 64];
   for (int i = tid; i < NS * 512 / 4; i += 256) ((unsigned*)hb)[i] = 0u;
-  float c[4][4];
+  LstmState st;
 #pragma unroll
   for (int ut = 0; ut < 4; ++ut)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) c[ut][r] = 0.f;
+    for (int r = 0; r < 4; ++r) st.c[ut][r] = 0.f;
 
   const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + 64 * w + (lane >> 4) * 4;
-  bf16x4 gn[4][4];
 #pragma unroll
   for (int ut = 0; ut < 4; ++ut)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) gn[ut][g] = *(const bf16x4*)(gxs + g * HD + ut * 16);
+    for (int g = 0; g < 4; ++g) st.gn[ut][g] = *(const bf16x4*)(gxs + g * HD + ut * 16);
   __syncthreads();
 
+  KPre pa, pb;
   for (int t = 0; t < Tn; ++t) {
     const bf16* gt = gxs + (int64_t)(t + 1 < Tn ? t + 1 : t) * G4;
-    float hv[4][4];
-    lstm_tile_step<0>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
-    lstm_tile_step<1>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
-    lstm_tile_step<2>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
-    lstm_tile_step<3>(gn, c, hv, gt, wa, wv, wl, hb, sl, lane);
-    __syncthreads();  // every wave has consumed h_{t-1}
+    kload<0>(pa, wl, hb, sl, lane);
+    ksteps<0>(st, pa, pb, gt, wa, wv, wl, hb, sl, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave has consumed h_{t-1} (no vmcnt drain: gx prefetch stays in flight)
 #pragma unroll
     for (int ut = 0; ut < 4; ++ut) {
       const int u = 64 * w + 16 * ut + (lane >> 4) * 4;
-      bf16x4 hv4 = {(bf16)hv[ut][0], (bf16)hv[ut][1], (bf16)hv[ut][2], (bf16)hv[ut][3]};
+      bf16x4 hv4 = {(bf16)st.hv[ut][0], (bf16)st.hv[ut][1], (bf16)st.hv[ut][2], (bf16)st.hv[ut][3]};
       *(bf16x4*)(hb + sl * 512 + (((u >> 3) ^ sl) << 4) + (u & 7) * 2) = hv4;
       if (valid) *(bf16x4*)(out + (int64_t)seq * out_seq_stride + (int64_t)t * HD + u) = hv4;
     }
-    __syncthreads();  // h_t visible to every wave
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // h_t visible to every wave
   }
 }
 

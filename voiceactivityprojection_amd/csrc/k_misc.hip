@@ -8,7 +8,7 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // conv0 (1 -> 256, k=10, s=5, p=3) -> ChannelNorm (unbiased var over 256 ch, eps 1e-5) -> ReLU
 // reference: vap/encoder_components.py:83-84 (conv0/batchNorm0), :62-70 (ChannelNorm), :99.
-// Block = 64 positions of one sequence; 4 threads per position, 64 channels each (registers),
+// Block = 64 positions of one sequence (seq = 2*clip + channel); 4 threads per position, 64 channels each (registers),
 // row stats by two 4-lane butterflies.  Output time-major [seq][2 + L0 + 2][256] (2 pad rows
 // each side = conv1's zero padding).
 // ------------------------------------------------------------------------------------------
@@ -33,12 +33,11 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ wa
     sb[2 * WROW + c + (c >> 6)] = bet[c];
   }
   __syncthreads();
-  const int s = blockIdx.y;          // sequence = ch * B + b
-  const int ch = s / B, b = s - ch * B;
+  const int s = blockIdx.y;  // sequence = 2 * clip + channel (clip-major == the [B][2][N] waveform)
   const int pos = blockIdx.x * 64 + (tid >> 2);
   const int q = tid & 3;
   if (pos >= L0) return;  // whole 4-lane groups exit together (shuffles stay within groups)
-  const float* src = wav + ((int64_t)b * 2 + ch) * N;
+  const float* src = wav + (int64_t)s * N;
   float smp[KW0];
   const int64_t i0 = (int64_t)pos * 5 - 3;
 #pragma unroll
@@ -120,15 +119,15 @@ __global__ __launch_bounds__(256) void vad_head_kernel(const float* __restrict__
                                                       const float* __restrict__ w, const float* __restrict__ bias,
                                                       float* __restrict__ vad) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over (c, b, t)
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over (seq = 2b + c, t)
   const int64_t rows = (int64_t)2 * B * Tn;
   if (row >= rows) return;
   const f32x4 v = *(const f32x4*)(x + row * 256 + lane * 4);
   const f32x4 ww = *(const f32x4*)(w + lane * 4);
   const float d = wave_sum(v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3]) + bias[0];
   if (lane == 0) {
-    const int64_t c = row / ((int64_t)B * Tn), bt = row - c * (int64_t)B * Tn;
-    vad[bt * 2 + c] = d;
+    const int64_t s = row / Tn, t = row - s * Tn;
+    vad[((s >> 1) * Tn + t) * 2 + (s & 1)] = d;
   }
 }
 

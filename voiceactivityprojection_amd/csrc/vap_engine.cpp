@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -47,12 +48,45 @@ struct vap_handle {
   std::map<std::string, void*> packed;  // storage-type buffers
   std::map<std::string, float*> fpacked;  // fp32 derived buffers (e.g. summed LSTM biases)
   bool finalized = false;
+  // micro-batch pipeline: side streams for the LSTM recurrences + events
+  static constexpr int NSIDE = 3, MAXMB = 16;
+  int microbatches = 4;
+  hipStream_t side[NSIDE] = {};
+  hipEvent_t mb_ev[MAXMB] = {};
+  hipEvent_t fork_ev[MAXMB] = {};
+  int fork_next = 0;
+  bool streams_ready = false;
+  int ensure_streams() {
+    if (streams_ready) return VAP_OK;
+    for (auto& s : side)
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return VAP_ERR_HIP;
+    for (int i = 0; i < MAXMB; ++i) {
+      if (hipEventCreateWithFlags(&mb_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
+      if (hipEventCreateWithFlags(&fork_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
+    }
+    streams_ready = true;
+    return VAP_OK;
+  }
+  // next fork event of the pool (recorded on the main stream, waited by a side stream); call ONCE
+  // per fork and use the returned handle for both the record and the wait
+  hipEvent_t next_fork_event() {
+    hipEvent_t e = fork_ev[fork_next];
+    fork_next = (fork_next + 1) % MAXMB;
+    return e;
+  }
   // timing hook
   int timing_cls = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
 
   ~vap_handle() {
+    if (streams_ready) {
+      for (auto& st : side) (void)hipStreamDestroy(st);
+      for (int i = 0; i < MAXMB; ++i) {
+        (void)hipEventDestroy(mb_ev[i]);
+        (void)hipEventDestroy(fork_ev[i]);
+      }
+    }
     for (auto& kv : params) (void)hipFree(kv.second.dev);
     for (auto& kv : packed) (void)hipFree(kv.second);
     for (auto& kv : fpacked) (void)hipFree(kv.second);
@@ -309,21 +343,38 @@ int pack_all(vap_handle* h, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------ forward
+// Sequences are CLIP-MAJOR: seq s = 2*clip + channel (speaker), matching the [B][2][N] waveform,
+// so a micro-batch of clips is one contiguous sequence range, and the stereo partner of s is s^1.
+struct Range {
+  int c0, nc;  // clips [c0, c0+nc)
+  int s0() const { return 2 * c0; }
+  int ns() const { return 2 * nc; }
+};
+
 template <typename T>
-int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, hipStream_t st) {
-  const int S = p.S, T_ = p.T;
+int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
+             hipStream_t st) {
+  const int T_ = p.T;
+  const int S = r.ns();
   const int64_t rows = (int64_t)S * T_;
-  float* X = (float*)(ws + p.X);
-  T* LN = (T*)(ws + p.LN);
-  T* RAW = (T*)(ws + p.RAW);
-  T* QKV = (T*)(ws + p.QKV);
-  T* KVC = (T*)(ws + p.KVC);
-  T* QC = (T*)(ws + p.QC);
-  T* ATT = (T*)(ws + p.ATT);
-  T* FF = (T*)(ws + p.FF);
+  const int64_t so = (int64_t)r.s0() * T_;  // row offset of the range
+  float* X = (float*)(ws + p.X) + so * D;
+  T* LN = (T*)(ws + p.LN) + so * D;
+  T* RAW = (T*)(ws + p.RAW) + so * D;
+  T* QKV = (T*)(ws + p.QKV) + so * 3 * D;
+  T* KVC = (T*)(ws + p.KVC) + so * 2 * D;
+  T* QC = (T*)(ws + p.QC) + so * D;
+  T* ATT = (T*)(ws + p.ATT) + so * D;
+  T* FF = (T*)(ws + p.FF) + so * 3 * D;
   const int H = h->dims.num_heads;
   const float scale = 1.0f / std::sqrt((float)D);
-  const bool f32out = false;
+  const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
+  auto resid = [&](GemmArgs g) {
+    g.add = X;
+    g.ld_add = D;
+    g.add_seq_stride = t1;
+    return g;
+  };
   {
     Timed tm(h, VAP_K_NORM, st);
     HIPCHK(launch_layernorm<T>(X, rows, h->P(pre + ".ln_self_attn.weight"), h->P(pre + ".ln_self_attn.bias"), 1e-5f, LN,
@@ -331,25 +382,19 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(gemm<T>(gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".qkv"), D, 3 * D, nullptr, T_, S, QKV, 3 * D,
-                         (int64_t)T_ * 3 * D), st, f32out));
-    if (cross)
-      HIPCHK(gemm<T>(gargs(RAW, D, (int64_t)T_ * D, h->W<T>(pre + ".kvc"), D, 2 * D, nullptr, T_, S, KVC, 2 * D,
-                           (int64_t)T_ * 2 * D), st, f32out));
+    HIPCHK(gemm<T>(gargs(LN, D, t1, h->W<T>(pre + ".qkv"), D, 3 * D, nullptr, T_, S, QKV, 3 * D, t3), st, false));
+    if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
+      HIPCHK(gemm<T>(gargs(RAW, D, t1, h->W<T>(pre + ".kvc"), D, 2 * D, nullptr, T_, S, KVC, 2 * D, t2), st, false));
   }
   {
     Timed tm(h, VAP_K_ATTN, st);
-    AttnArgs a{QKV, 3 * D, (int64_t)T_ * 3 * D, QKV + D, 3 * D, (int64_t)T_ * 3 * D, QKV + 2 * D, 3 * D,
-               (int64_t)T_ * 3 * D, ATT, D, (int64_t)T_ * D, h->P(pre + ".mha.m"), S, T_, H, 0, scale};
+    AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, T_, H,
+               0, scale};
     HIPCHK(launch_attention<T>(a, st));
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    GemmArgs g = gargs(ATT, D, (int64_t)T_ * D, h->W<T>(pre + ".o"), D, D, nullptr, T_, S, X, D, (int64_t)T_ * D);
-    g.add = X;
-    g.ld_add = D;
-    g.add_seq_stride = (int64_t)T_ * D;
-    HIPCHK(gemm<T>(g, st, true));
+    HIPCHK(gemm<T>(resid(gargs(ATT, D, t1, h->W<T>(pre + ".o"), D, D, nullptr, T_, S, X, D, t1)), st, true));
   }
   if (cross) {
     {
@@ -359,22 +404,17 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(gemm<T>(gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".qc"), D, D, nullptr, T_, S, QC, D, (int64_t)T_ * D),
-                     st, f32out));
+      HIPCHK(gemm<T>(gargs(LN, D, t1, h->W<T>(pre + ".qc"), D, D, nullptr, T_, S, QC, D, t1), st, false));
     }
     {
       Timed tm(h, VAP_K_ATTN, st);
-      AttnArgs a{QC, D, (int64_t)T_ * D, KVC, 2 * D, (int64_t)T_ * 2 * D, KVC + D, 2 * D, (int64_t)T_ * 2 * D,
-                 ATT, D, (int64_t)T_ * D, h->P(pre + ".mha_cross.m"), S, T_, H, p.B, scale};
+      AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, T_, H, 1,
+                 scale};
       HIPCHK(launch_attention<T>(a, st));
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
-      GemmArgs g = gargs(ATT, D, (int64_t)T_ * D, h->W<T>(pre + ".oc"), D, D, nullptr, T_, S, X, D, (int64_t)T_ * D);
-      g.add = X;
-      g.ld_add = D;
-      g.add_seq_stride = (int64_t)T_ * D;
-      HIPCHK(gemm<T>(g, st, true));
+      HIPCHK(gemm<T>(resid(gargs(ATT, D, t1, h->W<T>(pre + ".oc"), D, D, nullptr, T_, S, X, D, t1)), st, true));
     }
   }
   {
@@ -384,55 +424,33 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    GemmArgs g = gargs(LN, D, (int64_t)T_ * D, h->W<T>(pre + ".w1"), D, 3 * D, nullptr, T_, S, FF, 3 * D,
-                       (int64_t)T_ * 3 * D);
+    GemmArgs g = gargs(LN, D, t1, h->W<T>(pre + ".w1"), D, 3 * D, nullptr, T_, S, FF, 3 * D, t3);
     g.act = 2;
-    HIPCHK(gemm<T>(g, st, f32out));
-    GemmArgs g2 = gargs(FF, 3 * D, (int64_t)T_ * 3 * D, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D,
-                        (int64_t)T_ * D);
-    g2.add = X;
-    g2.ld_add = D;
-    g2.add_seq_stride = (int64_t)T_ * D;
-    HIPCHK(gemm<T>(g2, st, true));
+    HIPCHK(gemm<T>(g, st, false));
+    HIPCHK(gemm<T>(resid(gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1)), st, true));
   }
   return VAP_OK;
 }
 
+// Front end of a clip range: conv0..conv4 (+ChannelNorm+ReLU) and the LSTM input projection of
+// layer 0.  All on `st`.
 template <typename T>
-int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits, float* vadl, unsigned char* ws,
-                hipStream_t st, float* enc_out = nullptr) {
-  const Plan p = make_plan(B, N, sizeof(T));
-  const int S = p.S, T_ = p.T;
+int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigned char* ws, Range r, hipStream_t st) {
+  const int S = r.ns();
   const int64_t* L = p.L;
-  T* X0 = (T*)(ws + p.X0);
-  T* X1 = (T*)(ws + p.X1);
-  T* X2 = (T*)(ws + p.X2);
-  T* X3 = (T*)(ws + p.X3);
-  T* X4 = (T*)(ws + p.X4);
-  float* GX = (float*)(ws + p.GX);
-  T* Hb[2] = {(T*)(ws + p.H0), (T*)(ws + p.H1)};
-  float* X = (float*)(ws + p.X);
   const std::string g = "encoder.encoder.gEncoder";
-
-  // pad rows (conv zero padding lives in explicit rows)
-  HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
-  HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
-  T* Xs[4] = {X1, X2, X3, X4};
+  T* X0 = (T*)(ws + p.X0) + r.s0() * p.s0;
+  T* Xs[4] = {(T*)(ws + p.X1) + r.s0() * p.s1, (T*)(ws + p.X2) + r.s0() * p.s2, (T*)(ws + p.X3) + r.s0() * p.s3,
+              (T*)(ws + p.X4) + r.s0() * p.s4};
   const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
-  for (int i = 0; i < 4; ++i) {
-    HIPCHK(launch_zero_rows<T>(Xs[i], S, ss[i], 1, st));
-    HIPCHK(launch_zero_rows<T>(Xs[i] + (L[i + 1] + 1) * D, S, ss[i], 1, st));
-  }
-  HIPCHK(launch_zero_rows<T>(Hb[0], S, p.sh, 4, st));
-  HIPCHK(launch_zero_rows<T>(Hb[1], S, p.sh, 4, st));
-
   {  // conv0 + CN0 + ReLU  (encoder_components.py:99)
     Timed tm(h, VAP_K_CONV0, st);
-    HIPCHK(launch_conv0<T>(wav, B, N, (int)L[0], h->P(g + ".conv0.weight"), h->P(g + ".conv0.bias"),
-                           h->P(g + ".batchNorm0.weight"), h->P(g + ".batchNorm0.bias"), X0, p.s0, st));
+    HIPCHK(launch_conv0<T>(wav + (int64_t)r.s0() * N, r.nc, N, (int)L[0], h->P(g + ".conv0.weight"),
+                           h->P(g + ".conv0.bias"), h->P(g + ".batchNorm0.weight"), h->P(g + ".batchNorm0.bias"), X0,
+                           p.s0, st));
   }
   // conv1..conv4 as implicit GEMMs with ChannelNorm + ReLU epilogue (encoder_components.py:100-103)
-  const T* ins[4] = {X0, X1, X2, X3};
+  const T* ins[4] = {X0, Xs[0], Xs[1], Xs[2]};
   const int64_t in_ss[4] = {p.s0, p.s1, p.s2, p.s3};
   const int lda[4] = {4 * D, 2 * D, 2 * D, 2 * D};
   const int Ks[4] = {8 * D, 4 * D, 4 * D, 4 * D};
@@ -447,72 +465,154 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
     ga.beta = h->P(g + ".batchNorm" + c + ".bias");
     HIPCHK(gemm<T>(ga, st, false));
   }
-  // LSTM (encoder_components.py:140-159): input projection GEMM + serial recurrence per layer
-  const int NL = h->dims.lstm_layers;
-  for (int l = 0; l < NL; ++l) {
-    const std::string s = "_l" + std::to_string(l);
-    const T* in = l == 0 ? X4 + D : Hb[(l - 1) & 1] + 4 * D;
-    const int64_t in_seq = l == 0 ? p.s4 : p.sh;
-    // bf16 mode: gx stored bf16 and the recurrence runs with W_hh resident on the CU
-    constexpr bool bf = sizeof(T) == 2;
-    {
-      Timed tm(h, VAP_K_LSTM_PROJ, st);
-      HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L[4], S, GX,
-                           4 * D, L[4] * 4 * D), st, !bf));
-    }
-    {
-      Timed tm(h, VAP_K_LSTM_REC, st);
-      if constexpr (bf)
-        HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L[4], (const bf16*)h->W<T>("whh" + s),
-                                    (bf16*)(Hb[l & 1] + 4 * D), p.sh, st));
-      else
-        HIPCHK(launch_lstm<T>(GX, S, (int)L[4], h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, st));
-    }
+  return VAP_OK;
+}
+
+// LSTM layer l of a clip range: input projection GEMM on `st`, recurrence on `rec_st`
+// (bf16 mode: gx bf16, W_hh resident on the CU).
+template <typename T>
+int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, hipStream_t st, hipStream_t rec_st) {
+  const int S = r.ns();
+  const int64_t L4 = p.L[4];
+  const std::string s = "_l" + std::to_string(l);
+  T* X4 = (T*)(ws + p.X4) + r.s0() * p.s4;
+  T* Hb[2] = {(T*)(ws + p.H0) + r.s0() * p.sh, (T*)(ws + p.H1) + r.s0() * p.sh};
+  constexpr bool bf = sizeof(T) == 2;
+  void* GX = bf ? (void*)((bf16*)(ws + p.GX) + r.s0() * L4 * 4 * D) : (void*)((float*)(ws + p.GX) + r.s0() * L4 * 4 * D);
+  const T* in = l == 0 ? X4 + D : Hb[(l - 1) & 1] + 4 * D;
+  const int64_t in_seq = l == 0 ? p.s4 : p.sh;
+  {
+    Timed tm(h, VAP_K_LSTM_PROJ, st);
+    HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L4, S, GX, 4 * D,
+                         L4 * 4 * D), st, !bf));
   }
+  if (rec_st != st) {  // fork: the recurrence waits for the projection (ONE event from the pool)
+    hipEvent_t fork = h->next_fork_event();
+    HIPCHK(hipEventRecord(fork, st));
+    HIPCHK(hipStreamWaitEvent(rec_st, fork, 0));
+  }
+  {
+    Timed tm(h, VAP_K_LSTM_REC, rec_st);
+    if constexpr (bf)
+      HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L4, (const bf16*)h->W<T>("whh" + s),
+                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st));
+    else
+      HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
+  }
+  return VAP_OK;
+}
+
+// Back end of a clip range: downsample, transformer stack, combinator, heads.  On `st`.
+template <typename T>
+int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logits, float* vadl, float* enc_out,
+             hipStream_t st) {
+  const int S = r.ns(), T_ = p.T;
+  const int NL = h->dims.lstm_layers;
+  const int64_t t1 = (int64_t)T_ * D;
+  T* Hf = (T*)(ws + ((NL - 1) & 1 ? p.H1 : p.H0)) + r.s0() * p.sh;
+  float* X = (float*)(ws + p.X) + r.s0() * t1;
   {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
     Timed tm(h, VAP_K_DOWNSAMPLE, st);
-    GemmArgs ga = gargs(Hb[(NL - 1) & 1], 2 * D, p.sh, h->W<T>("down"), 5 * D, D, h->P("encoder.downsample.1.bias"), T_,
-                        S, X, D, (int64_t)T_ * D);
+    GemmArgs ga = gargs(Hf, 2 * D, p.sh, h->W<T>("down"), 5 * D, D, h->P("encoder.downsample.1.bias"), T_, S, X, D, t1);
     ga.norm = 2;
     ga.act = 2;
     ga.gamma = h->P("encoder.downsample.2.ln.weight");
     ga.beta = h->P("encoder.downsample.2.ln.bias");
     HIPCHK(gemm<T>(ga, st, true));
   }
-  if (enc_out) {  // EncoderCPC output of both speakers, [2][B][T][256] (channel-major)
-    HIPCHK(hipMemcpyAsync(enc_out, X, (size_t)S * T_ * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (enc_out) {  // EncoderCPC output, (x1, x2) = channel 0 / 1 -> enc_out [2][B][T][256]
+    const int64_t B = p.B;
+    for (int c = 0; c < 2; ++c)
+      HIPCHK(hipMemcpy2DAsync(enc_out + ((int64_t)c * B + r.c0) * t1, t1 * sizeof(float), X + c * t1,
+                              2 * t1 * sizeof(float), t1 * sizeof(float), r.nc, hipMemcpyDeviceToDevice, st));
     return VAP_OK;
   }
   int rc;
   for (int l = 0; l < h->dims.channel_layers; ++l)
-    if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, st))) return rc;
+    if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, r, st))) return rc;
   for (int l = 0; l < h->dims.cross_layers; ++l)
-    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, st))) return rc;
+    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, r, st))) return rc;
 
   // combinator (modules.py:434-449) + heads (model.py:257-261)
-  T* RAW = (T*)(ws + p.RAW);
-  float* HC = (float*)(ws + p.HC);
-  T* HCT = (T*)(ws + p.HCT);
+  T* RAW = (T*)(ws + p.RAW) + r.s0() * t1;
+  float* HC = (float*)(ws + p.HC) + r.c0 * t1;
+  T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
   {
     Timed tm(h, VAP_K_HEADS, st);
     HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
-    GemmArgs ga = gargs(RAW, D, (int64_t)T_ * D, h->W<T>("comb_a"), D, D, nullptr, T_, B, HC, D, (int64_t)T_ * D);
+    // channel-0 rows are the even sequences: stride 2*T*D over the clips of the range
+    GemmArgs ga = gargs(RAW, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, T_, r.nc, HC, D, t1);
     ga.norm = 2;
     ga.act = 2;
     ga.gamma = h->P("ar.combinator.ln.weight");
     ga.beta = h->P("ar.combinator.ln.bias");
     HIPCHK(gemm<T>(ga, st, true));
     GemmArgs gb = ga;
-    gb.A = RAW + (int64_t)B * T_ * D;
+    gb.A = RAW + t1;
     gb.W = h->W<T>("comb_b");
     gb.add = HC;
     gb.ld_add = D;
-    gb.add_seq_stride = (int64_t)T_ * D;
+    gb.add_seq_stride = t1;
     HIPCHK(gemm<T>(gb, st, true));
-    HIPCHK(launch_layernorm<T>(HC, (int64_t)B * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
-    HIPCHK(gemm<T>(gargs(HCT, D, (int64_t)T_ * D, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, B, logits, 256,
-                         (int64_t)T_ * 256), st, true));
-    HIPCHK(launch_vad_head(X, B, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"), vadl, st));
+    HIPCHK(launch_layernorm<T>(HC, (int64_t)r.nc * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
+    HIPCHK(gemm<T>(gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
+                         logits + r.c0 * (int64_t)T_ * 256, 256, (int64_t)T_ * 256), st, true));
+    HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
+                           vadl + r.c0 * (int64_t)T_ * 2, st));
+  }
+  return VAP_OK;
+}
+
+// VapGPT.forward (model.py:249-268).  Micro-batch pipeline: the batch is split into up to
+// `microbatches` clip ranges; each range's front end runs on the caller's stream, its LSTM
+// recurrence (a few CUs, serial over time) on a side stream, and its back end on the caller's
+// stream after an event -- so the recurrences overlap the convolutions of later ranges and the
+// transformer of earlier ones.  Every range writes disjoint workspace / output rows.
+template <typename T>
+int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits, float* vadl, unsigned char* ws,
+                hipStream_t st, float* enc_out = nullptr) {
+  const Plan p = make_plan(B, N, sizeof(T));
+  const int S = p.S;
+  const int64_t* L = p.L;
+  // pad rows (conv zero padding lives in explicit rows)
+  T* X0 = (T*)(ws + p.X0);
+  HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
+  HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
+  T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
+  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
+  for (int i = 0; i < 4; ++i) {
+    HIPCHK(launch_zero_rows<T>(Xs[i], S, ss[i], 1, st));
+    HIPCHK(launch_zero_rows<T>(Xs[i] + (L[i + 1] + 1) * D, S, ss[i], 1, st));
+  }
+  HIPCHK(launch_zero_rows<T>((T*)(ws + p.H0), S, p.sh, 4, st));
+  HIPCHK(launch_zero_rows<T>((T*)(ws + p.H1), S, p.sh, 4, st));
+
+  const int NL = h->dims.lstm_layers;
+  int m = h->microbatches < 1 ? 1 : h->microbatches;
+  if (m > B) m = B;
+  if (NL > 1) m = 1;  // stacked LSTMs: keep the simple serial schedule
+  std::vector<Range> rs;
+  for (int i = 0; i < m; ++i) {
+    const int c0 = (int)((int64_t)B * i / m), c1 = (int)((int64_t)B * (i + 1) / m);
+    if (c1 > c0) rs.push_back({c0, c1 - c0});
+  }
+  int rc;
+  if (rs.size() == 1) {
+    if ((rc = front_end<T>(h, p, wav, N, ws, rs[0], st))) return rc;
+    for (int l = 0; l < NL; ++l)
+      if ((rc = lstm_layer<T>(h, p, ws, l, rs[0], st, st))) return rc;
+    return back_end<T>(h, p, ws, rs[0], logits, vadl, enc_out, st);
+  }
+  if ((rc = h->ensure_streams())) return rc;
+  for (size_t i = 0; i < rs.size(); ++i) {
+    if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
+    hipStream_t side = h->side[i % vap_handle::NSIDE];
+    if ((rc = lstm_layer<T>(h, p, ws, 0, rs[i], st, side))) return rc;
+    HIPCHK(hipEventRecord(h->mb_ev[i], side));
+  }
+  for (size_t i = 0; i < rs.size(); ++i) {
+    HIPCHK(hipStreamWaitEvent(st, h->mb_ev[i], 0));
+    if ((rc = back_end<T>(h, p, ws, rs[i], logits, vadl, enc_out, st))) return rc;
   }
   return VAP_OK;
 }
@@ -541,6 +641,8 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
     return fail(VAP_ERR_INVALID, "bad precision");
   vap_handle* h = new vap_handle();
   h->dims = *dims;
+  if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
+  if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);
   for (auto& kv : h->params) {
     if (hipMalloc(&kv.second.dev, kv.second.numel * sizeof(float)) != hipSuccess) {

@@ -58,13 +58,13 @@ struct AttnArgs {
   void* O; int64_t o_ld, o_seq;
   const float* slopes;                    // [H]
   int S, T, H;
-  int kv_swap;                            // K/V sequence = (s + kv_swap) % S  (0 = self)
+  int kv_swap;                            // 0: self (K/V of s); 1: cross (K/V of s ^ 1, clip-major pairs)
   float scale;
 };
 template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
 
-// va_classifier on both towers: vad[b][t][c] = dot(x_c[b,t], w) + bias (x fp32, channel-major seqs)
+// va_classifier on both towers: vad[b][t][c] = dot(x[2b+c][t], w) + bias (x fp32, clip-major seqs)
 hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const float* bias, float* vad, hipStream_t st);
 
 hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
