@@ -197,3 +197,12 @@ def test_bf16_multi_workgroup_batch_invariance(m16, m32):
     for k in ("p_now", "p_future", "vad"):
         err = (full[k] - ref[k]).abs().max().item()
         assert err <= BF16_TOL[k], (k, err)
+
+
+def test_encoder_bf16_vs_reference(m16, golden):
+    """bf16 encoder (fused conv0->conv1, resident LSTM) against the reference's EncoderCPC taps."""
+    g = golden("short_clip")
+    x1, x2 = m16.encode_audio(torch.from_numpy(g["waveform"]).cuda())
+    for got, exp in ((x1, g["enc1"]), (x2, g["enc2"])):
+        err = (got.cpu().numpy() - exp).__abs__().max()
+        assert err < 0.08, f"bf16 encoder max abs err {err}"

@@ -1,0 +1,285 @@
+// Fused CPC conv0 -> ChannelNorm -> ReLU -> conv1 -> ChannelNorm -> ReLU (bf16 perf mode).
+//
+// Reference: CPCEncoder conv0/batchNorm0 and conv1/batchNorm1 (vap/encoder_components.py:83-86,
+// 99-100), ChannelNorm (:62-70, unbiased variance over the 256 channels).
+//
+// The conv0 activation (256 ch x 64000 positions per speaker per 20 s: 4.2 GB bf16 at batch 64) is
+// never written to HBM.  conv1 (k=8, s=4, p=2) output t reads conv0 positions 4t-2+j, j = 0..7.
+// Split j = r + 4h (phase r = 0..3, half h = 0..1): for a tile of 128 outputs [t0, t0+128) and a
+// phase r, the needed positions are G_r[i] = x0[4(t0+i) - 2 + r], i = 0..128, and output row i uses
+// G_r[i] (h = 0) and G_r[i+1] (h = 1).  Per phase the workgroup regenerates G_r (129 x 256 bf16) in
+// LDS and runs the 512-deep K slice (taps r and r+4) of the conv1 GEMM against W1 tiles streamed
+// from L2.  Every conv0 position is generated once per tile (plus one halo row per phase).
+//
+// conv0 itself runs on the MFMA: z^T[c][p] = sum_k A[c][k] S[k][p] with a K = 32 split-bf16 layout
+//   k  0..9 : A = w_hi[c],  S = s_hi[p]      k 10..19: A = w_hi[c], S = s_lo[p]
+//   k 20..29: A = w_lo[c],  S = s_hi[p]      k 30, 31: A = b_hi[c], b_lo[c],  S = 1
+// (~16-bit mantissa products; the dropped w_lo*s_lo term is ~2^-16 relative), with the ChannelNorm
+// folded in:  w = g*(W0 - mean_c W0), b = g*(b0 - mean_c b0)  so  x0 = relu(rstd_p * z + beta0).
+// rstd_p comes from the exact centred quadratic form  var = (s^T G s + 2 h.s + beta)/255,
+// G = Wc^T Wc (10x10), h = Wc^T bc, beta = bc.bc  (Wc, bc = centred conv0 weights / bias), so the
+// statistics need no pass over the 256 channels.  Padding positions (p < 0 or p >= L0) are zero rows.
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 256, GROWS = BM + 1, GROWB = 512;  // G image: 129 rows x 256 ch bf16
+constexpr int NPOS = 144;                                      // 9 position tiles of 16 (>= 129)
+constexpr int SVROW = 80;                                      // padded split-sample row (32 bf16 + pad)
+constexpr int BROWB = 128;                                     // W1 staging row: 64 k bf16
+constexpr int OFF_G = 0;
+constexpr int OFF_B = OFF_G + GROWS * GROWB;      // 66048
+constexpr int OFF_SV = OFF_B + 2 * BN * BROWB;    // + 65536
+constexpr int OFF_RS = OFF_SV + NPOS * SVROW;     // + 11520
+constexpr int LDS_BYTES = OFF_RS + NPOS * 4;      // + 576 = 143680
+
+VAP_DEV int gswz(int row, int c16) { return c16 ^ (row & 15); }      // 32 chunks per G row
+VAP_DEV int bswz(int row, int c) { return c ^ ((row >> 1) & 7); }    // 8 chunks per W1 staging row
+
+struct C0Stat {  // layout of the c0stat float array (host-computed at weight packing)
+  static constexpr int G = 0;     // 10x10 centred Gram matrix
+  static constexpr int H = 100;   // 10
+  static constexpr int BETA = 110;
+  static constexpr int N = 112;
+};
+
+__global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ wav, int64_t N, int L0, int L1,
+                                                    const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
+                                                    const float* __restrict__ beta0, const bf16* __restrict__ W1,
+                                                    const float* __restrict__ b1, const float* __restrict__ g1,
+                                                    const float* __restrict__ be1, bf16* __restrict__ out,
+                                                    int64_t out_seq_stride) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  unsigned char* G = smem + OFF_G;
+  unsigned char* Bt = smem + OFF_B;
+  unsigned char* SV = smem + OFF_SV;
+  float* RS = (float*)(smem + OFF_RS);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int s = blockIdx.y;
+  const int t0 = blockIdx.x * BM;
+  const float* src = wav + (int64_t)s * N;
+
+  // conv0 A fragments of this wave: channel tiles 2w, 2w+1 (row c, k = 8(lane>>4)..+7)
+  chunk16 a0f[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) a0f[j] = c0w[((2 * w + j) * 16 + (lane & 15)) * 4 + (lane >> 4)];
+  float bet[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bet[j][e] = beta0[(2 * w + j) * 16 + 4 * (lane >> 4) + e];
+
+  // W1 staging: 2048 chunks of 16 B per k-step (256 rows x 8), 4 per thread
+  const bf16* bptr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    bptr[i] = W1 + (int64_t)row * 2048 + c * 8;
+  }
+  chunk16 rb[4];
+  auto kbase = [](int q) {  // global k-step q (0..31): phase r = q>>3, half h = (q>>2)&1, sub (q&3)
+    const int r = q >> 3, hh = (q >> 2) & 1, kk = q & 3;
+    return (r + 4 * hh) * 256 + kk * 64;
+  };
+  auto gload = [&](int q) {
+    const int kb = kbase(q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + kb);
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* base = Bt + buf * BN * BROWB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      *(chunk16*)(base + row * BROWB + bswz(row, c) * 16) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  for (int r = 0; r < 4; ++r) {
+    // ---------------- (a) split sample vectors + ChannelNorm statistics for the phase positions
+    if (tid < NPOS) {
+      const int i = tid;
+      const int p = 4 * (t0 + i) - 2 + r;
+      const bool valid = i < GROWS && p >= 0 && p < L0;
+      float sm[10];
+      const int64_t i0 = (int64_t)p * 5 - 3;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const int64_t ix = i0 + k;
+        sm[k] = (valid && ix >= 0 && ix < N) ? src[ix] : 0.f;
+      }
+      bf16 hi[10], lo[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        hi[k] = (bf16)sm[k];
+        lo[k] = (bf16)(sm[k] - (float)hi[k]);
+      }
+      bf16x8 v0 = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
+      bf16x8 v1 = {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]};
+      bf16x8 v2 = {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]};
+      bf16x8 v3 = {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], (bf16)1.0f, (bf16)1.0f};
+      unsigned char* row = SV + i * SVROW;
+      *(bf16x8*)(row + 0) = v0;
+      *(bf16x8*)(row + 16) = v1;
+      *(bf16x8*)(row + 32) = v2;
+      *(bf16x8*)(row + 48) = v3;
+      // var * 255 = s^T G s + 2 h.s + beta  (centred, exact in exact arithmetic)
+      float q = c0stat[C0Stat::BETA];
+#pragma unroll
+      for (int a = 0; a < 10; ++a) {
+        float ga = 2.0f * c0stat[C0Stat::H + a];
+#pragma unroll
+        for (int b = 0; b < 10; ++b) ga = fmaf(c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
+        q = fmaf(ga, sm[a], q);
+      }
+      RS[i] = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : -1.0f;
+    }
+    __syncthreads();  // (also: every wave finished reading the previous phase's G)
+
+    // ---------------- (b) conv0 on the MFMA -> ChannelNorm/ReLU -> bf16 G image
+#pragma unroll
+    for (int pt = 0; pt < NPOS / 16; ++pt) {
+      const int prow = pt * 16 + (lane & 15);  // position row of this lane's column
+      const chunk16 bfr = *(const chunk16*)(SV + prow * SVROW + (lane >> 4) * 16);
+      const float rs = RS[prow];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        z = mfma_chunk<bf16>(a0f[j], bfr, z);
+        if (prow < GROWS) {
+          const int c = (2 * w + j) * 16 + 4 * (lane >> 4);  // 4 consecutive channels
+          bf16x4 o4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o4[e] = (bf16)(rs < 0.f ? 0.f : fmaxf(fmaf(rs, z[e], bet[j][e]), 0.f));
+          *(bf16x4*)(G + prow * GROWB + gswz(prow, c >> 3) * 16 + (c & 7) * 2) = o4;
+        }
+      }
+    }
+    // stage the first W1 tile of this phase
+    lstore(0);
+    __syncthreads();
+
+    // ---------------- (c) 8 k-steps of 64 over taps r (h = 0) and r + 4 (h = 1)
+    for (int kq = 0; kq < 8; ++kq) {
+      const int q = r * 8 + kq;
+      const int cur = kq & 1;
+      if (q + 1 < 32) gload(q + 1);
+      const int hh = kq >> 2, kk = kq & 3;
+      const unsigned char* bbase = Bt + cur * BN * BROWB;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        chunk16 af[4], bfr[4];
+        const int c16 = kk * 8 + sub * 4 + (lane >> 4);  // chunk within the 512-B G row
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 64 + i * 16 + (lane & 15) + hh;
+          af[i] = *(const chunk16*)(G + row * GROWB + gswz(row, c16) * 16);
+        }
+        const int cb = sub * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wn * 64 + j * 16 + (lane & 15);
+          bfr[j] = *(const chunk16*)(bbase + row * BROWB + bswz(row, cb) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<bf16>(af[i], bfr[j], acc[i][j]);
+      }
+      if (kq + 1 < 8) lstore(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  const int colb = wn * 64 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float b = b1[colb + j * 16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][j] += b;
+  }
+  float* red = (float*)Bt;  // [BM][4]
+  float mean[4][4], rstd[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float sum = acc[i][0][e] + acc[i][1][e] + acc[i][2][e] + acc[i][3][e];
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      sum += __shfl_xor(sum, 8, 64);
+      if ((lane & 15) == 0) red[(wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4 + wn] = sum;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4);
+      mean[i][e] = (pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / BN);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = acc[i][j][e] - mean[i][e];
+        ss += d * d;
+      }
+      ss += __shfl_xor(ss, 1, 64);
+      ss += __shfl_xor(ss, 2, 64);
+      ss += __shfl_xor(ss, 4, 64);
+      ss += __shfl_xor(ss, 8, 64);
+      if ((lane & 15) == 0) red[(wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4 + wn] = ss;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4);
+      rstd[i][e] = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
+    }
+  bf16* obase = out + (int64_t)s * out_seq_stride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
+      if (t >= L1) continue;
+      bf16* orow = obase + (int64_t)t * BN;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = colb + j * 16;
+        const float v = (acc[i][j][e] - mean[i][e]) * rstd[i][e] * g1[col] + be1[col];
+        orow[col] = (bf16)fmaxf(v, 0.f);
+      }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
+                         const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
+                         bf16* out, int64_t out_seq_stride, hipStream_t st) {
+  if (S <= 0 || L1 <= 0) return hipErrorInvalidValue;
+  dim3 grid((L1 + BM - 1) / BM, S);
+  hipLaunchKernelGGL(conv01_kernel, grid, dim3(512), 0, st, wav, N, L0, L1, (const chunk16*)c0w, c0stat, beta0, W1,
+                     b1, g1, be1, out, out_seq_stride);
+  return hipGetLastError();
+}

@@ -200,7 +200,7 @@ Plan make_plan(int B, int64_t N, size_t es) {
     o = align_up(o + bytes);
     return r;
   };
-  p.X0 = take(S * p.s0 * es);
+  p.X0 = take(es == 2 ? 0 : S * p.s0 * es);  // bf16 mode: conv0 is fused into conv1 (never materialised)
   p.X1 = take(S * p.s1 * es);
   p.X2 = take(S * p.s2 * es);
   p.X3 = take(S * p.s3 * es);
@@ -271,6 +271,82 @@ GemmArgs gargs(const void* A, int64_t lda, int64_t aseq, const void* W, int K, i
 }
 
 // ------------------------------------------------------------------------ packing
+uint16_t bf16_bits(float f) {  // round to nearest even
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf16_val(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// conv0 with ChannelNorm folded in (see k_conv01.hip): centred weights Wc = W0 - mean_c W0,
+// bc = b0 - mean_c b0; MFMA operand rows [g*Wc (hi), g*Wc (hi), g*Wc (lo), g*bc (hi), g*bc (lo)];
+// statistics G = Wc^T Wc, h = Wc^T bc, beta = bc.bc.  Computed once in double on the host.
+int pack_conv0_fused(vap_handle* h, hipStream_t st) {
+  const std::string g = "encoder.encoder.gEncoder";
+  std::vector<float> W0(D * 10), b0(D), ga(D);
+  HIPCHK(hipMemcpyAsync(W0.data(), h->P(g + ".conv0.weight"), W0.size() * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(b0.data(), h->P(g + ".conv0.bias"), D * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ga.data(), h->P(g + ".batchNorm0.weight"), D * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  double m[10] = {0}, mb = 0;
+  for (int c = 0; c < D; ++c) {
+    for (int k = 0; k < 10; ++k) m[k] += W0[c * 10 + k];
+    mb += b0[c];
+  }
+  for (int k = 0; k < 10; ++k) m[k] /= D;
+  mb /= D;
+  std::vector<double> Wc(D * 10), bc(D);
+  for (int c = 0; c < D; ++c) {
+    for (int k = 0; k < 10; ++k) Wc[c * 10 + k] = (double)W0[c * 10 + k] - m[k];
+    bc[c] = (double)b0[c] - mb;
+  }
+  std::vector<float> stat(112, 0.f);
+  for (int a = 0; a < 10; ++a) {
+    for (int b = 0; b < 10; ++b) {
+      double acc = 0;
+      for (int c = 0; c < D; ++c) acc += Wc[c * 10 + a] * Wc[c * 10 + b];
+      stat[a * 10 + b] = (float)acc;
+    }
+    double acc = 0;
+    for (int c = 0; c < D; ++c) acc += Wc[c * 10 + a] * bc[c];
+    stat[100 + a] = (float)acc;
+  }
+  double beta = 0;
+  for (int c = 0; c < D; ++c) beta += bc[c] * bc[c];
+  stat[110] = (float)beta;
+  std::vector<uint16_t> op(D * 32);
+  for (int c = 0; c < D; ++c) {
+    for (int k = 0; k < 10; ++k) {
+      const float wv = (float)(ga[c] * Wc[c * 10 + k]);
+      const uint16_t hi = bf16_bits(wv);
+      const uint16_t lo = bf16_bits(wv - bf16_val(hi));
+      op[c * 32 + k] = hi;
+      op[c * 32 + 10 + k] = hi;
+      op[c * 32 + 20 + k] = lo;
+    }
+    const float bv = (float)(ga[c] * bc[c]);
+    const uint16_t bh = bf16_bits(bv);
+    op[c * 32 + 30] = bh;
+    op[c * 32 + 31] = bf16_bits(bv - bf16_val(bh));
+  }
+  void* dop = nullptr;
+  float* dst = nullptr;
+  if (hipMalloc(&dop, op.size() * 2) != hipSuccess || hipMalloc(&dst, stat.size() * 4) != hipSuccess)
+    return fail(VAP_ERR_HIP, "hipMalloc conv0 operand");
+  h->packed["conv0_op"] = dop;
+  h->fpacked["conv0_stat"] = dst;
+  HIPCHK(hipMemcpyAsync(dop, op.data(), op.size() * 2, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dst, stat.data(), stat.size() * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return VAP_OK;
+}
+
 template <typename T>
 int pack_all(vap_handle* h, hipStream_t st) {
   auto alloc = [&](const std::string& name, int64_t n) -> T* {
@@ -281,6 +357,10 @@ int pack_all(vap_handle* h, hipStream_t st) {
   };
   const std::string g = "encoder.encoder.gEncoder";
   const int kws[5] = {10, 8, 4, 4, 4};
+  if constexpr (sizeof(T) == 2) {  // fused conv0 operand + ChannelNorm statistics (k_conv01.hip)
+    int rc = pack_conv0_fused(h, st);
+    if (rc) return rc;
+  }
   for (int i = 1; i < 5; ++i) {
     T* w = alloc("conv" + std::to_string(i), (int64_t)D * D * kws[i]);
     if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv");
@@ -443,7 +523,15 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   T* Xs[4] = {(T*)(ws + p.X1) + r.s0() * p.s1, (T*)(ws + p.X2) + r.s0() * p.s2, (T*)(ws + p.X3) + r.s0() * p.s3,
               (T*)(ws + p.X4) + r.s0() * p.s4};
   const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
-  {  // conv0 + CN0 + ReLU  (encoder_components.py:99)
+  int first = 0;
+  if constexpr (sizeof(T) == 2) {  // fused conv0 -> CN0 -> ReLU -> conv1 -> CN1 -> ReLU (k_conv01.hip)
+    Timed tm(h, VAP_K_CONV1, st);
+    HIPCHK(launch_conv01(wav + (int64_t)r.s0() * N, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"),
+                         h->fpacked.at("conv0_stat"), h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"),
+                         h->P(g + ".conv1.bias"), h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"),
+                         (bf16*)(Xs[0] + D), p.s1, st));
+    first = 1;
+  } else {  // conv0 + CN0 + ReLU  (encoder_components.py:99), then conv1 as an implicit GEMM
     Timed tm(h, VAP_K_CONV0, st);
     HIPCHK(launch_conv0<T>(wav + (int64_t)r.s0() * N, r.nc, N, (int)L[0], h->P(g + ".conv0.weight"),
                            h->P(g + ".conv0.bias"), h->P(g + ".batchNorm0.weight"), h->P(g + ".batchNorm0.bias"), X0,
@@ -454,7 +542,7 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   const int64_t in_ss[4] = {p.s0, p.s1, p.s2, p.s3};
   const int lda[4] = {4 * D, 2 * D, 2 * D, 2 * D};
   const int Ks[4] = {8 * D, 4 * D, 4 * D, 4 * D};
-  for (int i = 0; i < 4; ++i) {
+  for (int i = first; i < 4; ++i) {
     const std::string c = std::to_string(i + 1);
     Timed tm(h, i == 0 ? VAP_K_CONV1 : VAP_K_CONV234, st);
     GemmArgs ga = gargs(ins[i], lda[i], in_ss[i], h->W<T>("conv" + c), Ks[i], D, h->P(g + ".conv" + c + ".bias"),
@@ -575,9 +663,11 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   const int S = p.S;
   const int64_t* L = p.L;
   // pad rows (conv zero padding lives in explicit rows)
-  T* X0 = (T*)(ws + p.X0);
-  HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
-  HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
+  if constexpr (sizeof(T) == 4) {  // bf16 mode never materialises conv0
+    T* X0 = (T*)(ws + p.X0);
+    HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
+    HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
+  }
   T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
   const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
   for (int i = 0; i < 4; ++i) {

@@ -87,3 +87,9 @@ hipError_t launch_aggregate(const float* probs, int64_t frames, int nb, int from
 // VapGPT.vad post-processing: (p >= cutoff) -> fill silences <= max_fill -> omit spikes <= max_omit
 hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, int max_fill, int max_omit, float* out,
                            hipStream_t st);
+
+// bf16 perf mode: fused conv0 -> CN0 -> ReLU -> conv1 -> CN1 -> ReLU (k_conv01.hip).
+// c0w: [256][32] bf16 split-bf16 conv0 operand; c0stat: centred Gram statistics (112 floats).
+hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
+                         const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
+                         bf16* out, int64_t out_seq_stride, hipStream_t st);
