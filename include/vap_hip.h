@@ -130,6 +130,10 @@ int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, co
 int vap_test_probe_mfma_f32(const float* a, const float* b, float* d, void* stream);
 int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
                        void* raw, void* stream);
+/* row-panel projection GEMM (bf16 perf path, K = 256): amode 0 bf16 A / 1 fp32 A + LayerNorm /
+ * 2 fp32 A raw; epi 0 bf16 out / 1 GELU bf16 out / 2 fp32 out + residual `add` (ld = ldc). */
+int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
+                      const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
 
 #ifdef __cplusplus
 }

@@ -199,3 +199,42 @@ def test_layernorm(prec):
     tol = 1e-5 if prec == "fp32" else 2e-2
     assert (out.float().cpu() - ref).abs().max().item() <= tol
     assert (raw.float().cpu() - x.to(dt).float()).abs().max().item() == 0
+
+
+@pytest.mark.parametrize("amode,epi,N", [(1, 0, 768), (1, 0, 256), (1, 1, 1024), (2, 0, 512), (0, 2, 256)])
+@pytest.mark.parametrize("M", [1, 77, 1000])
+def test_rowpanel(amode, epi, N, M):
+    """Row-panel projection GEMM (bf16 perf path): LN / raw fp32 / bf16 A panel, bf16 / GELU /
+    fp32+residual epilogue, ragged last panel."""
+    L = lib()
+    D = 256
+    g = torch.Generator().manual_seed(11 + M + N)
+    x = torch.randn(M, D, generator=g) * 2 + 0.5
+    ga = 1 + 0.2 * torch.randn(D, generator=g)
+    be = 0.1 * torch.randn(D, generator=g)
+    W = (torch.randn(N, D, generator=g) / 16).to(torch.bfloat16)
+    add = torch.randn(M, N, generator=g) if epi == 2 else None
+    A = x.to(torch.bfloat16) if amode == 0 else x
+    dA, dW, dga, dbe = A.cuda(), W.cuda(), ga.cuda(), be.cuda()
+    dadd = add.cuda() if add is not None else None
+    C = torch.zeros(M, N, device="cuda", dtype=torch.float32 if epi == 2 else torch.bfloat16)
+    _run(L.lib().vap_test_rowpanel, _p(dA), D, M, _p(dW), D, N, _p(C), N, _p(dadd),
+         _p(dga) if amode == 1 else None, _p(dbe) if amode == 1 else None, amode, epi, _st())
+    a = F.layer_norm(x, (D,), ga, be) if amode == 1 else x
+    ref = a.to(torch.bfloat16).float() @ W.float().t()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = ref + add
+    err = (C.float().cpu() - ref).abs().max().item()
+    tol = 1e-4 if epi == 2 else 2e-2  # fp32 output: accumulation order only; bf16 output rounding
+    assert err <= tol * max(1.0, ref.abs().max().item()), f"rowpanel({amode},{epi},{N}) M={M}: {err}"
+
+
+def test_rowpanel_rejects_bad_shapes():
+    L = lib()
+    z = torch.zeros(64, 256, device="cuda")
+    W = torch.zeros(200, 256, device="cuda", dtype=torch.bfloat16)
+    C = torch.zeros(64, 200, device="cuda", dtype=torch.bfloat16)
+    rc = L.lib().vap_test_rowpanel(_p(z), 256, 64, _p(W), 256, 200, _p(C), 200, None, None, None, 2, 0, _st())
+    assert rc != 0

@@ -1,0 +1,206 @@
+// Row-panel GEMM for the transformer projections (bf16 perf mode), K = 256.
+//
+//   C[m, n] = epi( sum_k A'[m, k] W[n, k] ),   A' = LayerNorm(x[m]) | x[m] (fp32 -> bf16) | A[m] (bf16)
+//
+// Reference ops: the pre-LN TransformerLayer projections (vap/modules.py:246-275): LN_sa -> Q/K/V,
+// raw src -> cross K/V, LN_src -> cross Q, attention output -> proj (+ residual), LN_ff -> FFN up
+// (GELU).  K = dim = 256, so a 64-row A panel (32 KiB bf16) stays resident in LDS while EVERY
+// 256-wide N tile of W streams past it: the activation is read once (not once per N tile) and the
+// LayerNorm is computed while the panel is loaded (no LN kernel, no normalised copy in HBM).
+// Operands are swapped (C^T[n][m] = W[n] . A[m]) so each lane owns 4 consecutive outputs of one
+// row: 8-byte bf16 / 16-byte fp32 stores, 16-byte residual reads.
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+// 64-row panels, 4 waves, W streamed in 32-deep k-steps: 64 KiB LDS -> two workgroups per CU, so
+// one workgroup's panel load / stores overlap the other's MFMAs (a single resident workgroup
+// serialises load -> compute -> store and leaves HBM or the matrix pipes idle).
+constexpr int BM = 64, BN = 256, KP = 256, PROWB = KP * 2;  // A panel row: 512 B
+constexpr int BK = 32, WROWB = BK * 2;                      // W staging row: 64 B
+constexpr int OFF_W = BM * PROWB;                           // 32 KiB
+constexpr int LDS_BYTES = OFF_W + 2 * BN * WROWB;           // + 32 KiB
+constexpr int KSTEPS = KP / BK;                             // 8 per N tile
+constexpr int NPF = 4;                                      // W prefetch depth (k-steps)
+
+VAP_DEV int pswz(int row, int c16) { return c16 ^ (row & 15); }
+VAP_DEV int wswz(int row, int c) { return c ^ ((row >> 2) & 2); }  // 64-B rows: b128 reads + writes conflict-free
+
+template <int AMODE, int EPI>
+__global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  unsigned char* P = smem;
+  unsigned char* Wt = smem + OFF_W;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;  // wave w: columns w*64..+63 of the N tile
+  const int nsteps = (g.N / BN) * KSTEPS;
+  const int m0 = blockIdx.x * BM;
+  const bf16* __restrict__ W = (const bf16*)g.W;
+
+  // W staging: 1024 chunks per k-step, 4 per thread.  NPF register sets: the load for k-step
+  // q + NPF is issued at step q, so an L2 round trip is hidden behind NPF steps of MFMAs.
+  chunk16 rb[NPF][4];
+  auto gload = [&](int q, chunk16* r) {
+    const int nt = q / KSTEPS, k0 = (q % KSTEPS) * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 256, row = id >> 2, c = id & 3;
+      r[i] = *(const chunk16*)(W + (int64_t)(nt * BN + row) * KP + k0 + c * 8);
+    }
+  };
+  auto lstore = [&](int buf, const chunk16* r) {
+    unsigned char* base = Wt + buf * BN * WROWB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 256, row = id >> 2, c = id & 3;
+      *(chunk16*)(base + row * WROWB + wswz(row, c) * 16) = r[i];
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < NPF; ++p) gload(p, rb[p]);
+
+  // ------------------------------------------------------------ A panel -> LDS (bf16)
+  if constexpr (AMODE == 0) {  // bf16 rows: 64 x 512 B = 2048 chunks, 8 per thread
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int id = tid + i * 256, row = id >> 5, c = id & 31;
+      const int m = m0 + row;
+      const chunk16 v = m < g.M ? *(const chunk16*)((const bf16*)g.A + (int64_t)m * g.lda + c * 8) : chunk16{0, 0, 0, 0};
+      *(chunk16*)(P + row * PROWB + pswz(row, c) * 16) = v;
+    }
+  } else {
+    // fp32 rows (+ LayerNorm).  Wave w owns rows w*16 .. w*16+15 as 4 sets of 4; in one load
+    // instruction each 16-lane group reads 256 contiguous bytes of its row (2 full lines), so the
+    // panel streams at line granularity.  Lane (r4 = lane>>4, cc = lane&15) holds floats
+    // jj*64 + cc*4 .. +3 (jj = 0..3) of row w*16 + set*4 + r4; row statistics reduce over the
+    // 16-lane group.
+    const int r4 = lane >> 4, cc = lane & 15;
+    f32x4 v[4][4];
+#pragma unroll
+    for (int set = 0; set < 4; ++set) {
+      const int m = m0 + w * 16 + set * 4 + r4;
+      const float* src = (const float*)g.A + (int64_t)(m < g.M ? m : 0) * g.lda + cc * 4;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) v[set][jj] = m < g.M ? *(const f32x4*)(src + jj * 64) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (AMODE == 1) {
+      f32x4 ga[4], be[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        ga[jj] = *(const f32x4*)(g.gamma + jj * 64 + cc * 4);
+        be[jj] = *(const f32x4*)(g.beta + jj * 64 + cc * 4);
+      }
+#pragma unroll
+      for (int set = 0; set < 4; ++set) {
+        float sum = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sum += v[set][jj][0] + v[set][jj][1] + v[set][jj][2] + v[set][jj][3];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+        const float mean = sum * (1.0f / KP);
+        float ss = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[set][jj] -= mean;
+          ss += v[set][jj][0] * v[set][jj][0] + v[set][jj][1] * v[set][jj][1] + v[set][jj][2] * v[set][jj][2] +
+                v[set][jj][3] * v[set][jj][3];
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o, 64);
+        const float rstd = rsqrtf(ss * (1.0f / KP) + g.eps);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) v[set][jj] = v[set][jj] * rstd * ga[jj] + be[jj];
+      }
+    }
+#pragma unroll
+    for (int set = 0; set < 4; ++set) {
+      const int row = w * 16 + set * 4 + r4;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {  // 8 bytes = half of 16-byte chunk jj*8 + cc/2
+        const bf16x4 b = {(bf16)v[set][jj][0], (bf16)v[set][jj][1], (bf16)v[set][jj][2], (bf16)v[set][jj][3]};
+        *(bf16x4*)(P + row * PROWB + pswz(row, jj * 8 + (cc >> 1)) * 16 + (cc & 1) * 8) = b;
+      }
+    }
+  }
+  lstore(0, rb[0]);
+  __syncthreads();
+
+  // ------------------------------------------------------------ N tiles x k-steps
+  f32x4 acc[4][4];  // [n tile 16][m tile 16] of C^T
+  // nsteps is a multiple of KSTEPS (8), hence of NPF: unrolling by NPF makes every register-set
+  // index static.
+  for (int q0 = 0; q0 < nsteps; q0 += NPF) {
+#pragma unroll
+    for (int p = 0; p < NPF; ++p) {
+      const int q = q0 + p;
+      const int kq = q % KSTEPS;
+      if (kq == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      const unsigned char* wb = Wt + (q & 1) * BN * WROWB;
+      chunk16 wf[4], af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = w * 64 + i * 16 + (lane & 15);
+        wf[i] = *(const chunk16*)(wb + row * WROWB + wswz(row, lane >> 4) * 16);
+      }
+      const int ca = kq * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = j * 16 + (lane & 15);
+        af[j] = *(const chunk16*)(P + row * PROWB + pswz(row, ca) * 16);
+      }
+      if (q + NPF < nsteps) gload(q + NPF, rb[p]);  // set p held step q: stored at step q-1
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<bf16>(wf[i], af[j], acc[i][j]);
+      if (q + 1 < nsteps) lstore((q + 1) & 1, rb[(p + 1) % NPF]);
+      if (kq == KSTEPS - 1) {
+        // epilogue of N tile nt: lane owns C[m][n .. n+3]
+        const int nt = q / KSTEPS;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + j * 16 + (lane & 15);
+          if (m >= g.M) continue;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int n = nt * BN + w * 64 + i * 16 + (lane >> 4) * 4;
+            f32x4 v = acc[i][j];
+            if constexpr (EPI == 1) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+            }
+            if constexpr (EPI == 2) {
+              float* c = (float*)g.C + (int64_t)m * g.ldc + n;
+              v += *(const f32x4*)((const float*)g.add + (int64_t)m * g.ldc + n);
+              *(f32x4*)c = v;
+            } else {
+              store4((bf16*)g.C + (int64_t)m * g.ldc + n, v[0], v[1], v[2], v[3]);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st) {
+  if (g.M <= 0 || g.N % BN != 0 || g.K != KP) return hipErrorInvalidValue;
+  const dim3 grid((g.M + BM - 1) / BM);
+#define RP_LAUNCH(A, E) hipLaunchKernelGGL((rowpanel_kernel<A, E>), grid, dim3(256), 0, st, g)
+  if (amode == 0 && epi == 0) RP_LAUNCH(0, 0);
+  else if (amode == 0 && epi == 2) RP_LAUNCH(0, 2);
+  else if (amode == 1 && epi == 0) RP_LAUNCH(1, 0);
+  else if (amode == 1 && epi == 1) RP_LAUNCH(1, 1);
+  else if (amode == 2 && epi == 0) RP_LAUNCH(2, 0);
+  else return hipErrorInvalidValue;
+#undef RP_LAUNCH
+  return hipGetLastError();
+}

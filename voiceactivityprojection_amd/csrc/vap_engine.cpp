@@ -51,6 +51,7 @@ struct vap_handle {
   // micro-batch pipeline: side streams for the LSTM recurrences + events
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
+  bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
   hipStream_t side[NSIDE] = {};
   hipEvent_t mb_ev[MAXMB] = {};
   hipEvent_t fork_ev[MAXMB] = {};
@@ -431,9 +432,80 @@ struct Range {
   int ns() const { return 2 * nc; }
 };
 
+// bf16 transformer layer on row-panel kernels: LayerNorm fused into the A-panel load of the
+// Q/K/V, cross-Q and FFN-up projections; residual adds fused into the output projections.
+int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
+                hipStream_t st) {
+  using T = bf16;
+  const int T_ = p.T;
+  const int S = r.ns();
+  const int rows = S * T_;
+  const int64_t so = (int64_t)r.s0() * T_;
+  float* X = (float*)(ws + p.X) + so * D;
+  T* QKV = (T*)(ws + p.QKV) + so * 3 * D;
+  T* KVC = (T*)(ws + p.KVC) + so * 2 * D;
+  T* QC = (T*)(ws + p.QC) + so * D;
+  T* ATT = (T*)(ws + p.ATT) + so * D;
+  T* FF = (T*)(ws + p.FF) + so * 3 * D;
+  const int H = h->dims.num_heads;
+  const float scale = 1.0f / std::sqrt((float)D);
+  const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
+  auto rp = [&](const void* A, int64_t lda, const std::string& w, int N, void* C, int64_t ldc, const float* add,
+                const std::string& ln, int amode, int epi) {
+    RowPanelArgs a{A, lda, rows, h->W<T>(w), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
+                   ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
+    return launch_rowpanel(a, amode, epi, st);
+  };
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(X, D, pre + ".qkv", 3 * D, QKV, 3 * D, nullptr, pre + ".ln_self_attn", 1, 0));
+    if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
+      HIPCHK(rp(X, D, pre + ".kvc", 2 * D, KVC, 2 * D, nullptr, "", 2, 0));
+  }
+  {
+    Timed tm(h, VAP_K_ATTN, st);
+    AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, T_, H,
+               0, scale};
+    HIPCHK(launch_attention<T>(a, st));
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(ATT, D, pre + ".o", D, X, D, X, "", 0, 2));
+  }
+  if (cross) {
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      HIPCHK(rp(X, D, pre + ".qc", D, QC, D, nullptr, pre + ".ln_src_attn", 1, 0));
+    }
+    {
+      Timed tm(h, VAP_K_ATTN, st);
+      AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, T_, H, 1,
+                 scale};
+      HIPCHK(launch_attention<T>(a, st));
+    }
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      HIPCHK(rp(ATT, D, pre + ".oc", D, X, D, X, "", 0, 2));
+    }
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(X, D, pre + ".w1", 3 * D, FF, 3 * D, nullptr, pre + ".ln_ffnetwork", 1, 1));
+    GemmArgs g2 = gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1);
+    g2.add = X;
+    g2.ld_add = D;
+    g2.add_seq_stride = t1;
+    HIPCHK(gemm<T>(g2, st, true));
+  }
+  return VAP_OK;
+}
+
 template <typename T>
 int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
              hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (!h->legacy_tr) return tr_layer_rp(h, p, ws, pre, cross, r, st);
+  }
   const int T_ = p.T;
   const int S = r.ns();
   const int64_t rows = (int64_t)S * T_;
@@ -732,6 +804,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   vap_handle* h = new vap_handle();
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
+  if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);
   for (auto& kv : h->params) {

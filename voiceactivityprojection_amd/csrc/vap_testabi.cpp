@@ -108,4 +108,13 @@ int vap_test_layernorm(int precision, const float* x, int64_t rows, const float*
   return rc_of(launch_layernorm<float>(x, rows, gamma, beta, 1e-5f, (float*)out, (float*)raw, st));
 }
 
+int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
+                      const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream) {
+  RowPanelArgs g{};
+  g.A = A; g.lda = lda; g.M = M; g.W = W; g.K = K; g.N = N; g.C = C; g.ldc = ldc;
+  g.add = add; g.gamma = gamma; g.beta = beta; g.eps = 1e-5f;
+  if ((amode == 1) != (gamma != nullptr && beta != nullptr) || (epi == 2) != (add != nullptr)) return VAP_ERR_INVALID;
+  return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
+}
+
 }  // extern "C"
