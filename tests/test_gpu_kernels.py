@@ -201,7 +201,7 @@ def test_layernorm(prec):
     assert (raw.float().cpu() - x.to(dt).float()).abs().max().item() == 0
 
 
-@pytest.mark.parametrize("amode,epi,N", [(1, 0, 768), (1, 0, 256), (1, 1, 1024), (2, 0, 512), (0, 2, 256)])
+@pytest.mark.parametrize("amode,epi,N", [(1, 0, 768), (1, 0, 256), (1, 1, 768), (2, 0, 512), (0, 2, 256)])
 @pytest.mark.parametrize("M", [1, 77, 1000])
 def test_rowpanel(amode, epi, N, M):
     """Row-panel projection GEMM (bf16 perf path): LN / raw fp32 / bf16 A panel, bf16 / GELU /

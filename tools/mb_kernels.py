@@ -48,7 +48,7 @@ def main():
     beta = (0.1 * torch.randn(D, generator=g)).to(dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
-    for name, amode, epi, N in [("qkv_ln", 1, 0, 768), ("q_ln", 1, 0, 256), ("ff1_ln_gelu", 1, 1, 1024),
+    for name, amode, epi, N in [("qkv_ln", 1, 0, 768), ("q_ln", 1, 0, 256), ("ff1_ln_gelu", 1, 1, 768),
                                 ("kv_raw", 2, 0, 512), ("proj_resid", 0, 2, 256)]:
         W = (torch.randn(N, D, generator=g) / 16).to(dev).to(torch.bfloat16)
         A = xb if amode == 0 else x
