@@ -33,10 +33,44 @@ def timeit(fn, iters):
     return a.elapsed_time(b) * 1e3 / iters  # us
 
 
+def bench_attn(lib, dev, st, iters, S=32, T=1000, H=4):
+    """Causal AliBi attention at the engine's layout: Q/K/V columns of one [S][T][768] bf16 buffer."""
+    g = torch.Generator(device="cpu").manual_seed(1)
+    qkv = (torch.randn(S, T, 768, generator=g) * 2).to(torch.bfloat16).to(dev)
+    O = torch.empty(S, T, 256, device=dev, dtype=torch.bfloat16)
+    slopes = torch.tensor([0.25, 0.0625, 0.015625, 0.00390625], device=dev)
+    scale = 1.0 / 16
+    res = {}
+    for kv_swap in (0, 1):
+        def run():
+            _native.check(lib.vap_test_attention(1, ctypes.c_void_p(qkv.data_ptr()), 768, T * 768,
+                                                 ctypes.c_void_p(qkv.data_ptr() + 512), 768, T * 768,
+                                                 ctypes.c_void_p(qkv.data_ptr() + 1024), 768, T * 768,
+                                                 ptr(O), 256, T * 256, ptr(slopes), S, T, H, kv_swap,
+                                                 ctypes.c_float(scale), st))
+        us = timeit(run, iters)
+        # reference on 4 sequences (fp32 math on the bf16 inputs)
+        q = qkv[:4, :, :256].float().view(4, T, H, 64).transpose(1, 2)
+        src = qkv[[1, 0, 3, 2]] if kv_swap else qkv[:4]
+        k = src[:, :, 256:512].float().view(4, T, H, 64).transpose(1, 2)
+        v = src[:, :, 512:].float().view(4, T, H, 64).transpose(1, 2)
+        i = torch.arange(T, device=dev)
+        bias = slopes.view(H, 1, 1) * (i.view(1, 1, T) - i.view(1, T, 1)).float()
+        bias = bias.masked_fill(i.view(1, 1, T) > i.view(1, T, 1), float("-inf"))
+        att = torch.softmax(q @ k.transpose(-1, -2) * scale + bias, -1) @ v
+        ref = att.transpose(1, 2).reshape(4, T, 256)
+        err = (O[:4].float() - ref).abs().max().item()
+        flops = S * H * (T * (T + 1) / 2) * 64 * 4
+        res[f"attn_kv{kv_swap}"] = dict(us=round(us, 2), tflops=round(flops / us / 1e6, 1), max_err=round(err, 4))
+        print(f"attn_kv{kv_swap}", res[f"attn_kv{kv_swap}"], flush=True)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32000)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--which", default="rowpanel,attn")
     args = ap.parse_args()
     lib = _native.lib()
     dev = torch.device("cuda:0")
@@ -48,6 +82,11 @@ def main():
     beta = (0.1 * torch.randn(D, generator=g)).to(dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
+    if "attn" in args.which:
+        res.update(bench_attn(lib, dev, st, args.iters))
+    if "rowpanel" not in args.which:
+        print(json.dumps(res))
+        return
     for name, amode, epi, N in [("qkv_ln", 1, 0, 768), ("q_ln", 1, 0, 256), ("ff1_ln_gelu", 1, 1, 768),
                                 ("kv_raw", 2, 0, 512), ("proj_resid", 0, 2, 256)]:
         W = (torch.randn(N, D, generator=g) / 16).to(dev).to(torch.bfloat16)

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -71,4 +73,16 @@ VAP_DEV void store4(float* p, float a, float b, float c, float d) { *(f32x4*)p =
 VAP_DEV void store4(bf16* p, float a, float b, float c, float d) {
   bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
   *(bf16x4*)p = v;
+}
+
+// Buffer resource over [p, p + bytes) for raw buffer loads: out-of-range reads return 0 (the
+// hardware range check replaces per-lane bounds branches).  p and bytes must be wave-uniform.
+VAP_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pu = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pu, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+VAP_DEV chunk16 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(chunk16, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
