@@ -232,7 +232,7 @@ VAP_DEV void ksteps(LstmState& st, KPre& cur, KPre& nxt, const bf16* gt, const c
 
 __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __restrict__ gx, int S, int Tn,
                                                               const chunk16* __restrict__ wp, bf16* __restrict__ out,
-                                                              int64_t out_seq_stride) {
+                                                              int64_t out_seq_stride, LstmSync sync) {
   __shared__ __attribute__((aligned(16))) chunk16 wls[R_NW * R_NLDS * 64];
   __shared__ __attribute__((aligned(16))) unsigned char hb[NS * 512];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -250,6 +250,30 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
 #pragma unroll
   for (int f = 0; f < R_NLDS; ++f) wl[f * 64] = wsrc[(R_NREG + f) * 64];
   for (int i = tid; i < NS * 512 / 4; i += 256) ((unsigned*)hb)[i] = 0u;
+  // ranges covered by this workgroup's sequences (persistent multi-range launch)
+  int ra = 0, rb = -1;
+  if (sync.ready) {
+    const int s_first = blockIdx.x * NS, s_last = min(S, s_first + NS) - 1;
+    while (sync.seq_end[ra] <= s_first) ++ra;
+    rb = ra;
+    while (sync.seq_end[rb] <= s_last) ++rb;
+    if (tid == 0) {
+      // the producer stream publishes ready[r] after the range's gate projection completed; a
+      // system-scope acquire also invalidates this CU's and XCD's caches for the gx reads below
+      // bounded: after ~2 s (100 MHz s_memrealtime) give up, flag the error word and run on, so a
+      // lost flag can never hang the device (done counters are still published below)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (int r = ra; r <= rb; ++r)
+        while (__hip_atomic_load(sync.ready + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < sync.epoch) {
+          __builtin_amdgcn_s_sleep(8);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+    }
+    __syncthreads();
+  }
   LstmState st;
 #pragma unroll
   for (int ut = 0; ut < 4; ++ut)
@@ -279,6 +303,12 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // h_t visible to every wave
+  }
+  if (sync.ready) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's h stores are complete
+    __syncthreads();
+    if (tid == 0)  // release: the consumer stream's kernels (any XCD) see every h of these ranges
+      for (int r = ra; r <= rb; ++r) __hip_atomic_fetch_add(sync.done + r, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -315,10 +345,15 @@ hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st) {
 }
 
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
-                                int64_t out_seq_stride, hipStream_t st) {
+                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync) {
   if (S <= 0 || Tn <= 0) return hipErrorInvalidValue;
+  LstmSync sy{};
+  if (sync) {
+    if (sync->nr < 1 || sync->nr > 16 || sync->seq_end[sync->nr - 1] < S) return hipErrorInvalidValue;
+    sy = *sync;
+  }
   hipLaunchKernelGGL(lstm_resident_kernel, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
-                     (const chunk16*)whh_packed, out, out_seq_stride);
+                     (const chunk16*)whh_packed, out, out_seq_stride, sy);
   return hipGetLastError();
 }
 hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st) {

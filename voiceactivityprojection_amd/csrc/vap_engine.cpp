@@ -57,6 +57,13 @@ struct vap_handle {
   hipEvent_t fork_ev[MAXMB] = {};
   int fork_next = 0;
   bool streams_ready = false;
+  // persistent-LSTM hand-off (bf16): ready[MAXMB] then done[MAXMB] counters in device memory,
+  // monotonic across calls (epoch / cumulative expectations kept here)
+  unsigned* sync_mem = nullptr;
+  unsigned epoch = 0;
+  unsigned done_expect[MAXMB] = {};
+  bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
+  bool persistent_lstm = true;  // VAP_PERSISTENT_LSTM=0: one LSTM launch per range on the side streams
   int ensure_streams() {
     if (streams_ready) return VAP_OK;
     for (auto& s : side)
@@ -64,6 +71,13 @@ struct vap_handle {
     for (int i = 0; i < MAXMB; ++i) {
       if (hipEventCreateWithFlags(&mb_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
       if (hipEventCreateWithFlags(&fork_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
+    }
+    int dev = 0, wv = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && wv) {
+      if (hipMalloc(&sync_mem, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
+      if (hipMemset(sync_mem, 0, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
+      wait_value = true;
     }
     streams_ready = true;
     return VAP_OK;
@@ -82,6 +96,7 @@ struct vap_handle {
 
   ~vap_handle() {
     if (streams_ready) {
+      if (sync_mem) (void)hipFree(sync_mem);
       for (auto& st : side) (void)hipStreamDestroy(st);
       for (int i = 0; i < MAXMB; ++i) {
         (void)hipEventDestroy(mb_ev[i]);
@@ -631,7 +646,8 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
 // LSTM layer l of a clip range: input projection GEMM on `st`, recurrence on `rec_st`
 // (bf16 mode: gx bf16, W_hh resident on the CU).
 template <typename T>
-int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, hipStream_t st, hipStream_t rec_st) {
+int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, hipStream_t st, hipStream_t rec_st,
+               bool recurrence = true) {
   const int S = r.ns();
   const int64_t L4 = p.L[4];
   const std::string s = "_l" + std::to_string(l);
@@ -646,6 +662,7 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
     HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L4, S, GX, 4 * D,
                          L4 * 4 * D), st, !bf));
   }
+  if (!recurrence) return VAP_OK;
   if (rec_st != st) {  // fork: the recurrence waits for the projection (ONE event from the pool)
     hipEvent_t fork = h->next_fork_event();
     HIPCHK(hipEventRecord(fork, st));
@@ -655,7 +672,7 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
     Timed tm(h, VAP_K_LSTM_REC, rec_st);
     if constexpr (bf)
       HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L4, (const bf16*)h->W<T>("whh" + s),
-                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st));
+                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr));
     else
       HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
   }
@@ -766,6 +783,51 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
     return back_end<T>(h, p, ws, rs[0], logits, vadl, enc_out, st);
   }
   if ((rc = h->ensure_streams())) return rc;
+  if constexpr (sizeof(T) == 2) {
+    if (h->wait_value && h->persistent_lstm) {
+      // One persistent LSTM launch on a side stream covers every range: its workgroups start as
+      // each range's gate projection lands (ready flag written by this stream) and publish done
+      // counters the back ends wait on.  No per-range launches, so no range queues behind another
+      // range's recurrence on a shared side stream.
+      const int nr = (int)rs.size();
+      LstmSync sy{};
+      sy.ready = h->sync_mem;
+      sy.done = h->sync_mem + vap_handle::MAXMB;
+      sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
+      sy.epoch = ++h->epoch;
+      sy.nr = nr;
+      for (int i = 0; i < nr; ++i) sy.seq_end[i] = 2 * (rs[i].c0 + rs[i].nc);
+      for (int wg = 0; wg * 16 < S; ++wg) {  // done increments per range (launch_lstm_resident: 16 sequences per WG)
+        const int s_first = wg * 16, s_last = std::min(S, s_first + 16) - 1;
+        int ra = 0;
+        while (sy.seq_end[ra] <= s_first) ++ra;
+        int rb = ra;
+        while (sy.seq_end[rb] <= s_last) ++rb;
+        for (int r = ra; r <= rb; ++r) ++h->done_expect[r];
+      }
+      hipStream_t side = h->side[0];
+      hipEvent_t fork = h->next_fork_event();
+      HIPCHK(hipEventRecord(fork, st));
+      HIPCHK(hipStreamWaitEvent(side, fork, 0));
+      {
+        Timed tm(h, VAP_K_LSTM_REC, side);
+        HIPCHK(launch_lstm_resident((const bf16*)(ws + p.GX), S, (int)L[4], (const bf16*)h->W<T>("whh_l0"),
+                                    (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh, side, &sy));
+      }
+      for (int i = 0; i < nr; ++i) {
+        if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
+        if ((rc = lstm_layer<T>(h, p, ws, 0, rs[i], st, st, false))) return rc;
+        HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + i), sy.epoch, 0));
+      }
+      for (int i = 0; i < nr; ++i) {
+        HIPCHK(hipStreamWaitValue32(st, sy.done + i, h->done_expect[i], hipStreamWaitValueGte, 0xFFFFFFFFu));
+        if ((rc = back_end<T>(h, p, ws, rs[i], logits, vadl, enc_out, st))) return rc;
+      }
+      HIPCHK(hipEventRecord(h->mb_ev[0], side));  // join: the launch has fully retired
+      HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
+      return VAP_OK;
+    }
+  }
   for (size_t i = 0; i < rs.size(); ++i) {
     if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
     hipStream_t side = h->side[i % vap_handle::NSIDE];
@@ -805,6 +867,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
   if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
+  if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);
   for (auto& kv : h->params) {

@@ -47,8 +47,20 @@ hipError_t launch_lstm(const float* gx, int S, int Tn, const T* whh_packed, T* o
 template <typename T>
 hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st);
 // bf16 perf mode: W_hh resident in VGPRs + LDS (8 waves / CU), gx in bf16 [S][T][1024]
+// Cross-stream hand-off for a single persistent LSTM launch covering several clip ranges: a
+// workgroup waits until ready[r] >= epoch for the ranges r its 16 sequences fall in (written by the
+// producing stream after the range's input projection), and on completion adds 1 to done[r] for
+// each of them (the consuming stream waits for its expected count).  ready == nullptr: no hand-off.
+struct LstmSync {
+  const unsigned* ready;
+  unsigned* done;
+  unsigned* error;   // set to 1 if a ready flag did not arrive within ~2 s (never expected)
+  unsigned epoch;
+  int nr;            // number of ranges
+  int seq_end[16];   // exclusive end sequence of each range
+};
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
-                                int64_t out_seq_stride, hipStream_t st);
+                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync);
 hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st);
 
 struct AttnArgs {

@@ -78,7 +78,7 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
   if (precision == VAP_PRECISION_BF16 && variant == 0) {
     hipError_t e = launch_pack_whh_resident(whh, (bf16*)whh_packed, st);
     if (e != hipSuccess) return VAP_ERR_HIP;
-    return rc_of(launch_lstm_resident((const bf16*)gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st));
+    return rc_of(launch_lstm_resident((const bf16*)gx, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr));
   }
   if (precision == VAP_PRECISION_BF16) {
     hipError_t e = launch_pack_whh<bf16>(whh, (bf16*)whh_packed, st);
