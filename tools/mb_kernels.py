@@ -7,6 +7,7 @@ transformer projection kernels at the bench's per-range shape (32 sequences x 10
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 
@@ -66,11 +67,58 @@ def bench_attn(lib, dev, st, iters, S=32, T=1000, H=4):
     return res
 
 
+def bench_gemm(lib, dev, st, iters, only=""):
+    """Generic implicit-conv GEMM (bf16) at the front-end / FFN shapes of one range (32 sequences)."""
+    g = torch.Generator(device="cpu").manual_seed(2)
+    res = {}
+    D = 256
+    gamma = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(D, generator=g)).to(dev)
+    bias = (0.1 * torch.randn(4 * D, generator=g)).to(dev)
+    # (name, rows_in_per_seq, lda, K, N, M_per_seq, norm, act, out_f32, residual)
+    cases = [("conv2_cn_relu", 16002, 512, 1024, 256, 8000, 1, 1, 0, 0),
+             ("conv2_plain", 16002, 512, 1024, 256, 8000, 0, 0, 0, 0),
+             ("conv3_cn_relu", 8002, 512, 1024, 256, 4000, 1, 1, 0, 0),
+             ("lstm_proj", 2000, 256, 256, 1024, 2000, 0, 0, 0, 0),
+             ("ff2_resid", 1000, 768, 768, 256, 1000, 0, 0, 1, 1)]
+    S = 32
+    for name, rin, lda, K, N, M, norm, act, out_f32, resid in cases:
+        if only and only not in name:
+            continue
+        A = (torch.randn(S, rin, lda if lda > D else D, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+        a_seq = A.shape[1] * A.shape[2]
+        W = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+        C = torch.empty(S, M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        add = torch.randn(S, M, N, generator=g).to(dev) if resid else None
+
+        def run():
+            _native.check(lib.vap_test_gemm(1, ptr(A), lda, a_seq, ptr(W), K, N, ptr(bias) if name == "lstm_proj" else None,
+                                            M, S, ptr(C), N, M * N, ptr(add), N, M * N,
+                                            ptr(gamma) if norm else None, ptr(beta) if norm else None,
+                                            norm, act, out_f32, st))
+        us = timeit(run, iters)
+        flops = 2.0 * S * M * N * K
+        res[name] = dict(us=round(us, 2), tflops=round(flops / us / 1e6, 1))
+        print(name, res[name], flush=True)
+    # reference point for the shape (timing only): hipBLASLt via torch.matmul, plain GEMM
+    if not only or only == "ref":
+        for name, M, K, N in [("ref_hipblaslt_256000x1024x256", 256000, 1024, 256),
+                              ("ref_hipblaslt_64000x256x1024", 64000, 256, 1024),
+                              ("ref_hipblaslt_8192x8192x8192", 8192, 8192, 8192)]:
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+            us = timeit(lambda: torch.matmul(a, w.t()), max(3, iters // 5))
+            res[name] = dict(us=round(us, 2), tflops=round(2.0 * M * N * K / us / 1e6, 1))
+            print(name, res[name], flush=True)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32000)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--which", default="rowpanel,attn")
+    ap.add_argument("--case", default="", help="only GEMM cases whose name contains this")
     args = ap.parse_args()
     lib = _native.lib()
     dev = torch.device("cuda:0")
@@ -84,6 +132,8 @@ def main():
     res = {}
     if "attn" in args.which:
         res.update(bench_attn(lib, dev, st, args.iters))
+    if "gemm" in args.which:
+        res.update(bench_gemm(lib, dev, st, args.iters, args.case))
     if "rowpanel" not in args.which:
         print(json.dumps(res))
         return

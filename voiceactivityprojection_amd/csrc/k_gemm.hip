@@ -18,6 +18,8 @@
 // Tile 128 x 256, 8 waves (2 along M x 4 along N, 64x64 per wave = 4x4 MFMA 16x16 tiles),
 // K staged 128 bytes per row per step (64 bf16 / 32 f32) through a double-buffered, XOR-swizzled
 // LDS image (chunk ^= (row>>1)&7 : conflict-free ds_read_b128 for 16 consecutive rows).
+#include <cstdlib>
+
 #include "vap_common.h"
 #include "vap_kernels.h"
 
@@ -232,6 +234,16 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   constexpr int BK = 8 * (16 / sizeof(T));
   if (g.K % BK != 0 || g.N % BN != 0 || M <= 0) return hipErrorInvalidValue;
   if (g.norm && g.N != BN) return hipErrorInvalidValue;
+  if constexpr (sizeof(T) == 2) {
+    static const bool v1 = getenv("VAP_GEMM_V1") != nullptr;
+    const bool aligned = !(g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 ||
+                           (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)));
+    // 256-row tiles when they still fill the chip (~one workgroup per CU) or the K loop is long
+    // enough to amortise the deeper prologue; short-K small-M launches (combinator / heads of a
+    // range) keep 128-row tiles for twice the workgroups
+    const bool big = (int64_t)((M + 255) / 256) * (g.N / BN) >= 200 || g.K >= 512;
+    if (!v1 && aligned && big) return launch_gemm2<TOut>(g, st);
+  }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);
   return hipGetLastError();

@@ -1,0 +1,243 @@
+// bf16 MFMA GEMM, 256 x 256 tiles, LDS-DMA staging (the bf16 perf path of launch_gemm).
+//
+// Same contract as gemm_kernel (k_gemm.hip): implicit-convolution A rows (lda may be < K, per
+// sequence strides), W [N][K], fused bias / ChannelNorm | LayerNorm / ReLU | GELU / fp32 residual
+// epilogue, bf16 or fp32 output.  Used for the CPC conv2..4 (k4 s2 implicit convs, K = 1024), the
+// LSTM input projection, the downsample conv (+LN+GELU), FFN-down (+residual), combinator and heads.
+//
+// Structure (MI355X):
+//   * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave:
+//     W is re-read from L2 once per 256 rows (not per 128), A once per tile;
+//   * K staged 32 deep (64-byte rows) by global_load_lds_dwordx4: 16 DMA pieces of 16 rows x 64 B
+//     per operand and stage, 2 + 2 per wave, no VGPR staging.  The LDS image is lane-linear, the
+//     XOR swizzle (conflict-free ds_read_b128 for 16 consecutive rows) is applied to the SOURCE
+//     address and again on the fragment read;
+//   * four 32 KiB stages, DMA three stages ahead (96 KiB in flight; raw s_barrier, counted vmcnt —
+//     no __syncthreads, whose fence would drain them), and ping-pong scheduling of the two waves
+//     that share each SIMD (one reads fragments while the other runs its MFMAs);
+//   * operands swapped (C^T = W A^T) so a lane owns 4 consecutive columns of one row: 8-byte bf16 /
+//     16-byte fp32 stores and residual loads, row statistics by a 16-lane-stride shuffle + LDS.
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 32, ROWB = 64;  // BK bf16 = 64 B per staged row
+constexpr int NST = 4;                                  // stages: 3 in flight while one computes
+constexpr int STAGE = (BM + BN) * ROWB;                 // 32 KiB
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 64-byte rows, 4 chunks: conflict-free ds_read_b128 for 16 consecutive rows x 4 chunks
+VAP_DEV int swz(int row, int c) { return c ^ ((row >> 2) & 2); }
+
+template <typename TOut>
+__global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int M = g.M_per_seq * g.n_seq;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const bf16* __restrict__ A = (const bf16*)g.A;
+  const bf16* __restrict__ W = (const bf16*)g.W;
+
+  // DMA sources: a piece (one wave instruction, 1 KiB) = 16 rows x 64 B; wave w fills pieces 2w and
+  // 2w+1 of each operand image; lane -> (row 16p + lane/4, physical chunk lane%4) holding logical
+  // chunk (lane%4) ^ swz(row).  32-bit byte offsets from the uniform operand bases (saddr+voffset).
+  uint32_t aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + (lane >> 2);
+    const int c = swz(row, lane & 3);
+    int m = m0 + row;
+    m = m < M ? m : M - 1;  // tail rows: any valid row (never stored)
+    const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+    aoff[i] = (uint32_t)(((int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * 8) * 2);
+    boff[i] = (uint32_t)(((int64_t)(n0 + row) * g.K + c * 8) * 2);
+  }
+  const unsigned char* Ab = (const unsigned char*)A;
+  const unsigned char* Wb = (const unsigned char*)W;
+  auto dma = [&](int kt) {
+    unsigned char* base = smem + (kt % NST) * STAGE;
+    const uint32_t kb = (uint32_t)kt * ROWB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(Ab + (aoff[i] + kb)), (lds_void*)(base + (wave * 2 + i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(Wb + (boff[i] + kb)), (lds_void*)(base + BM * ROWB + (wave * 2 + i) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[4][8];  // [n tile][m tile] of C^T
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (row-dependent part; the chunk varies with the k half)
+  const int fr = lane & 15, fc = lane >> 4;
+  const int nk = g.K / BK;
+  // Ping-pong: waves 0-3 and 4-7 (one of each per SIMD) run half a k-step apart.  Every k-step is
+  // a LOAD phase (issue the DMA three stages ahead, read this stage's fragments) and a COMPUTE phase
+  // (32 MFMAs), each closed by a workgroup barrier; group 1 enters one barrier late, so on every
+  // SIMD one wave's MFMAs overlap the other wave's LDS reads.
+  //   RAW: a wave waits (counted vmcnt) for its own DMA of stage t+1 at the end of COMPUTE t, before
+  //        the barrier that precedes any wave's first read of stage t+1.
+  //   WAR: stage t+3 overwrites stage t-1's buffer; its last reads (group 1's LOAD t-1) retire with
+  //        lgkmcnt(0) before the barrier that precedes group 0's LOAD t.
+  const int grp = wave >> 2;
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) dma(p);
+  if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    // ---- LOAD
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NST - 1 < nk) dma(kt + NST - 1);
+    const unsigned char* abase = smem + (kt % NST) * STAGE;
+    const unsigned char* bbase = abase + BM * ROWB;
+    chunk16 wf[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn * 64 + j * 16 + fr;
+      wf[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, fc) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wm * 128 + i * 16 + fr;
+      af[i] = *(const chunk16*)(abase + row * ROWB + swz(row, fc) * 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- COMPUTE
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = mfma_chunk<bf16>(wf[j], af[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // own DMA of stage kt+1 landed: newer DMAs are those of stages kt+2 and kt+3 (4 each, if issued)
+    if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---------------------------------------------------------------- epilogue
+  // lane holds C[m = m0 + wm*128 + i*16 + fr][n = n0 + wn*64 + j*16 + fc*4 + r]
+  const int nb = n0 + wn * 64 + fc * 4;
+  if (g.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 b = *(const f32x4*)(g.bias + nb + j * 16);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] += b;
+    }
+  }
+  if (g.norm) {
+    __syncthreads();  // all DMA retired (vmcnt(0) above) and every wave done reading the stages
+    float* red = (float*)smem;  // [BM][4 waves along N]
+    float mean[8], rstd[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fc == 0) red[(wm * 128 + i * 16 + fr) * 4 + wn] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 p = *(const f32x4*)(red + (wm * 128 + i * 16 + fr) * 4);
+      mean[i] = (p[0] + p[1] + p[2] + p[3]) * (1.0f / BN);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[j][i][r] - mean[i];
+          s += d * d;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fc == 0) red[(wm * 128 + i * 16 + fr) * 4 + wn] = s;
+    }
+    __syncthreads();
+    const float inv_n = g.norm == 1 ? 1.0f / (BN - 1) : 1.0f / BN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 p = *(const f32x4*)(red + (wm * 128 + i * 16 + fr) * 4);
+      rstd[i] = rsqrtf((p[0] + p[1] + p[2] + p[3]) * inv_n + g.eps);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 ga = *(const f32x4*)(g.gamma + nb + j * 16);
+      const f32x4 be = *(const f32x4*)(g.beta + nb + j * 16);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = (acc[j][i] - mean[i]) * rstd[i] * ga + be;
+    }
+  }
+  if (g.act == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][i][r] = fmaxf(acc[j][i][r], 0.f);
+  } else if (g.act == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[j][i][r] = gelu_erf(acc[j][i][r]);
+  }
+  TOut* __restrict__ C = (TOut*)g.C;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + fr;
+    if (m >= M) continue;
+    const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+    TOut* crow = C + (int64_t)s * g.c_seq_stride + (int64_t)t * g.ldc + nb;
+    const float* arow = g.add ? g.add + (int64_t)s * g.add_seq_stride + (int64_t)t * g.ld_add + nb : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 v = acc[j][i];
+      if (arow) v += *(const f32x4*)(arow + j * 16);
+      store4(crow + j * 16, v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+}  // namespace
+
+template <typename TOut>
+hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
+  const int M = g.M_per_seq * g.n_seq;
+  if (g.K % BK != 0 || g.N % BN != 0 || M <= 0) return hipErrorInvalidValue;
+  if (g.norm && g.N != BN) return hipErrorInvalidValue;
+  // 16-byte alignment of every DMA source / epilogue vector access
+  if (g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 || (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)))
+    return hipErrorInvalidValue;
+  dim3 grid((M + BM - 1) / BM, g.N / BN);
+  hipLaunchKernelGGL((gemm2_kernel<TOut>), grid, dim3(512), 0, st, g);
+  return hipGetLastError();
+}
+
+template hipError_t launch_gemm2<bf16>(const GemmArgs&, hipStream_t);
+template hipError_t launch_gemm2<float>(const GemmArgs&, hipStream_t);

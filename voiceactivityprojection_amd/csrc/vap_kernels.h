@@ -24,6 +24,9 @@ struct GemmArgs {
 
 template <typename T, typename TOut>
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+// bf16 256x256-tile LDS-DMA variant (k_gemm2.hip); launch_gemm<bf16, *> dispatches to it
+template <typename TOut>
+hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st);
 
 // conv0 (1 -> 256, k10 s5 p3) + ChannelNorm + ReLU, time-major output with pad rows.
 template <typename T>
