@@ -349,8 +349,8 @@ __global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
   constexpr float LOG2E = 1.4426950408889634f;
   constexpr float TAU = 8.0f;
   const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
-  const int qw0 = qb * QB2 + w * 32;  // first query of this wave
-  const int qlast = min(qb * QB2 + QB2 - 1, a.T - 1);
+  const int qw0 = a.q0 + qb * QB2 + w * 32;  // first query of this wave (absolute)
+  const int qlast = min(a.q0 + qb * QB2 + QB2 - 1, a.T - 1);
   const int nkb = qlast / KB2 + 1;
 
   chunk16 qf[2][2];
@@ -517,17 +517,20 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.T <= 0 || a.S <= 0 || a.H <= 0) return hipErrorInvalidValue;
   if constexpr (sizeof(T) == 2) {
     static const int ver = getenv("VAP_ATTN_V1") ? 1 : getenv("VAP_ATTN_V2") ? 2 : 3;
+    if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
     if (ver == 3) {
-      const int nqb = (a.T + QB2 - 1) / QB2;
+      const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
       hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
       return hipGetLastError();
     }
+    if (a.q0 != 0) return hipErrorInvalidValue;
     if (ver == 2) {
       dim3 grid((a.T + QB2 - 1) / QB2, a.H, a.S);
       hipLaunchKernelGGL(attn2_kernel, grid, dim3(256), 0, st, a);
       return hipGetLastError();
     }
   }
+  if (a.q0 != 0) return hipErrorInvalidValue;
   dim3 grid((a.T + QB - 1) / QB, a.H, a.S);
   hipLaunchKernelGGL((attn_kernel<T>), grid, dim3(256), 0, st, a);
   return hipGetLastError();

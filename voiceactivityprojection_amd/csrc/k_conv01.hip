@@ -49,7 +49,7 @@ __global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ w
                                                     const float* __restrict__ beta0, const bf16* __restrict__ W1,
                                                     const float* __restrict__ b1, const float* __restrict__ g1,
                                                     const float* __restrict__ be1, bf16* __restrict__ out,
-                                                    int64_t out_seq_stride) {
+                                                    int64_t out_seq_stride, int r0, int r1) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   unsigned char* G = smem + OFF_G;
   unsigned char* Bt = smem + OFF_B;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ w
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
   const int s = blockIdx.y;
-  const int t0 = blockIdx.x * BM;
+  const int t0 = r0 + blockIdx.x * BM;  // output rows [r0, r1) of conv1
   const float* src = wav + (int64_t)s * N;
 
   // conv0 A fragments of this wave: channel tiles 2w, 2w+1 (row c, k = 8(lane>>4)..+7)
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ w
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
-      if (t >= L1) continue;
+      if (t >= r1) continue;
       bf16* orow = obase + (int64_t)t * BN;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -276,10 +276,11 @@ __global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ w
 
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
                          const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
-                         bf16* out, int64_t out_seq_stride, hipStream_t st) {
-  if (S <= 0 || L1 <= 0) return hipErrorInvalidValue;
-  dim3 grid((L1 + BM - 1) / BM, S);
+                         bf16* out, int64_t out_seq_stride, hipStream_t st, int r0, int r1) {
+  if (r1 < 0) r1 = L1;
+  if (S <= 0 || L1 <= 0 || r0 < 0 || r1 > L1 || r0 >= r1) return hipErrorInvalidValue;
+  dim3 grid((r1 - r0 + BM - 1) / BM, S);
   hipLaunchKernelGGL(conv01_kernel, grid, dim3(512), 0, st, wav, N, L0, L1, (const chunk16*)c0w, c0stat, beta0, W1,
-                     b1, g1, be1, out, out_seq_stride);
+                     b1, g1, be1, out, out_seq_stride, r0, r1);
   return hipGetLastError();
 }

@@ -253,10 +253,14 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
   // ranges covered by this workgroup's sequences (persistent multi-range launch)
   int ra = 0, rb = -1;
   if (sync.ready) {
-    const int s_first = blockIdx.x * NS, s_last = min(S, s_first + NS) - 1;
-    while (sync.seq_end[ra] <= s_first) ++ra;
-    rb = ra;
-    while (sync.seq_end[rb] <= s_last) ++rb;
+    if (sync.time_mode) {
+      rb = 0;  // time chunks: the first chunk now, the others at their boundaries
+    } else {
+      const int s_first = blockIdx.x * NS, s_last = min(S, s_first + NS) - 1;
+      while (sync.seq_end[ra] <= s_first) ++ra;
+      rb = ra;
+      while (sync.seq_end[rb] <= s_last) ++rb;
+    }
     if (tid == 0) {
       // the producer stream publishes ready[r] after the range's gate projection completed; a
       // system-scope acquire also invalidates this CU's and XCD's caches for the gx reads below
@@ -288,6 +292,7 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
   __syncthreads();
 
   KPre pa, pb;
+  int chunk = 0;
   for (int t = 0; t < Tn; ++t) {
     const bf16* gt = gxs + (int64_t)(t + 1 < Tn ? t + 1 : t) * G4;
     kload<0>(pa, wl, hb, sl, lane);
@@ -303,8 +308,39 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // h_t visible to every wave
+    if (sync.time_mode && chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) {
+      // end of a time chunk: publish its h rows (every chunk ending here), then wait for the next
+      // chunk's gate projection
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int c0 = chunk;
+      while (chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) ++chunk;
+      if (tid == 0) {
+        for (int c = c0; c < chunk; ++c)
+          __hip_atomic_fetch_add(sync.done + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (chunk < sync.nr) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < sync.epoch) {
+            __builtin_amdgcn_s_sleep(8);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+              if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+          }
+        }
+      }
+      if (chunk < sync.nr) {
+        __syncthreads();
+        // the in-step prefetch of step t+1 may predate the projection: load it again
+        const bf16* gn1 = gxs + (int64_t)(t + 1) * G4;
+#pragma unroll
+        for (int ut = 0; ut < 4; ++ut)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) st.gn[ut][g] = *(const bf16x4*)(gn1 + g * HD + ut * 16);
+      }
+    }
   }
-  if (sync.ready) {
+  if (sync.ready && !sync.time_mode) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's h stores are complete
     __syncthreads();
     if (tid == 0)  // release: the consumer stream's kernels (any XCD) see every h of these ranges
@@ -349,7 +385,10 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
   if (S <= 0 || Tn <= 0) return hipErrorInvalidValue;
   LstmSync sy{};
   if (sync) {
-    if (sync->nr < 1 || sync->nr > 16 || sync->seq_end[sync->nr - 1] < S) return hipErrorInvalidValue;
+    if (sync->nr < 1 || sync->nr > 16 || sync->seq_end[sync->nr - 1] < (sync->time_mode ? Tn : S))
+      return hipErrorInvalidValue;
+    for (int c = 1; c < sync->nr; ++c)
+      if (sync->seq_end[c] <= sync->seq_end[c - 1]) return hipErrorInvalidValue;
     sy = *sync;
   }
   hipLaunchKernelGGL(lstm_resident_kernel, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,

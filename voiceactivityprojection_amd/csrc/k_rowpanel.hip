@@ -36,6 +36,17 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
   const int nsteps = (g.N / BN) * KSTEPS;
   const int m0 = blockIdx.x * BM;
   const bf16* __restrict__ W = (const bf16*)g.W;
+  // element offsets of row m in A and in C / add (contiguous rows, or a time chunk of each sequence)
+  auto aoff = [&](int m) -> int64_t {
+    if (g.rows_per_seq == 0) return (int64_t)m * g.lda;
+    const int sq = m / g.rows_per_seq;
+    return (int64_t)sq * g.a_seq + (int64_t)(m - sq * g.rows_per_seq) * g.lda;
+  };
+  auto coff = [&](int m) -> int64_t {
+    if (g.rows_per_seq == 0) return (int64_t)m * g.ldc;
+    const int sq = m / g.rows_per_seq;
+    return (int64_t)sq * g.c_seq + (int64_t)(m - sq * g.rows_per_seq) * g.ldc;
+  };
 
   // W staging: 1024 chunks per k-step, 4 per thread.  NPF register sets: the load for k-step
   // q + NPF is issued at step q, so an L2 round trip is hidden behind NPF steps of MFMAs.
@@ -65,7 +76,7 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
     for (int i = 0; i < 8; ++i) {
       const int id = tid + i * 256, row = id >> 5, c = id & 31;
       const int m = m0 + row;
-      const chunk16 v = m < g.M ? *(const chunk16*)((const bf16*)g.A + (int64_t)m * g.lda + c * 8) : chunk16{0, 0, 0, 0};
+      const chunk16 v = m < g.M ? *(const chunk16*)((const bf16*)g.A + aoff(m) + c * 8) : chunk16{0, 0, 0, 0};
       *(chunk16*)(P + row * PROWB + pswz(row, c) * 16) = v;
     }
   } else {
@@ -79,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
 #pragma unroll
     for (int set = 0; set < 4; ++set) {
       const int m = m0 + w * 16 + set * 4 + r4;
-      const float* src = (const float*)g.A + (int64_t)(m < g.M ? m : 0) * g.lda + cc * 4;
+      const float* src = (const float*)g.A + aoff(m < g.M ? m : 0) + cc * 4;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) v[set][jj] = m < g.M ? *(const f32x4*)(src + jj * 64) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -174,12 +185,12 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
             }
+            const int64_t co = coff(m) + n;
             if constexpr (EPI == 2) {
-              float* c = (float*)g.C + (int64_t)m * g.ldc + n;
-              v += *(const f32x4*)((const float*)g.add + (int64_t)m * g.ldc + n);
-              *(f32x4*)c = v;
+              v += *(const f32x4*)((const float*)g.add + co);
+              *(f32x4*)((float*)g.C + co) = v;
             } else {
-              store4((bf16*)g.C + (int64_t)m * g.ldc + n, v[0], v[1], v[2], v[3]);
+              store4((bf16*)g.C + co, v[0], v[1], v[2], v[3]);
             }
           }
         }

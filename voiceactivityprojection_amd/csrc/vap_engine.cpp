@@ -64,6 +64,10 @@ struct vap_handle {
   unsigned done_expect[MAXMB] = {};
   bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
   bool persistent_lstm = true;  // VAP_PERSISTENT_LSTM=0: one LSTM launch per range on the side streams
+  int time_chunks = 4;          // VAP_TIME_CHUNKS (bf16, 1-layer LSTM): pipeline the forward along time
+  bool use_time_chunks() const {
+    return dims.precision == VAP_PRECISION_BF16 && dims.lstm_layers == 1 && time_chunks >= 2;
+  }
   int ensure_streams() {
     if (streams_ready) return VAP_OK;
     for (auto& s : side)
@@ -193,11 +197,12 @@ struct Plan {
   int64_t L[6]{};
   int64_t s0, s1, s2, s3, s4, sh;  // per-sequence strides (elements) of padded activations
   size_t X0, X1, X2, X3, X4, GX, H0, H1, X, LN, RAW, QKV, KVC, QC, ATT, FF, HC, HCT, total;
+  size_t QKVL = 0, KVCL = 0;  // time-chunked mode: Q/K/V (self) and K/V (cross) of EVERY layer are kept
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
-Plan make_plan(int B, int64_t N, size_t es) {
+Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross_layers = 0) {
   Plan p;
   p.B = B;
   p.S = 2 * B;
@@ -234,8 +239,16 @@ Plan make_plan(int B, int64_t N, size_t es) {
   p.FF = take(S * T * 3 * D * es);
   p.HC = take((size_t)B * T * D * sizeof(float));
   p.HCT = take((size_t)B * T * D * es);
+  if (kv_self_layers) p.QKVL = take((size_t)kv_self_layers * S * T * 3 * D * es);
+  if (kv_cross_layers) p.KVCL = take((size_t)kv_cross_layers * S * T * 2 * D * es);
   p.total = o;
   return p;
+}
+
+Plan plan_for(const vap_handle* h, int B, int64_t N) {
+  const size_t es = h->dims.precision == VAP_PRECISION_BF16 ? 2 : 4;
+  const int nl = h->dims.channel_layers + h->dims.cross_layers;
+  return h->use_time_chunks() ? make_plan(B, N, es, nl, h->dims.cross_layers) : make_plan(B, N, es);
 }
 
 // ------------------------------------------------------------------------ timing hook
@@ -679,6 +692,43 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
   return VAP_OK;
 }
 
+// Combinator (modules.py:434-449) + heads (model.py:257-261) of a clip range, from the final
+// residual stream X.  On `st`.
+template <typename T>
+int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logits, float* vadl, hipStream_t st) {
+  const int S = r.ns(), T_ = p.T;
+  const int64_t t1 = (int64_t)T_ * D;
+  float* X = (float*)(ws + p.X) + r.s0() * t1;
+  T* RAW = (T*)(ws + p.RAW) + r.s0() * t1;
+  float* HC = (float*)(ws + p.HC) + r.c0 * t1;
+  T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
+  {
+    Timed tm(h, VAP_K_HEADS, st);
+    HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
+    // channel-0 rows are the even sequences: stride 2*T*D over the clips of the range
+    GemmArgs ga = gargs(RAW, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, T_, r.nc, HC, D, t1);
+    ga.norm = 2;
+    ga.act = 2;
+    ga.gamma = h->P("ar.combinator.ln.weight");
+    ga.beta = h->P("ar.combinator.ln.bias");
+    HIPCHK(gemm<T>(ga, st, true));
+    GemmArgs gb = ga;
+    gb.A = RAW + t1;
+    gb.W = h->W<T>("comb_b");
+    gb.add = HC;
+    gb.ld_add = D;
+    gb.add_seq_stride = t1;
+    HIPCHK(gemm<T>(gb, st, true));
+    HIPCHK(launch_layernorm<T>(HC, (int64_t)r.nc * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
+    HIPCHK(gemm<T>(gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
+                         logits + r.c0 * (int64_t)T_ * 256, 256, (int64_t)T_ * 256), st, true));
+    HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
+                           vadl + r.c0 * (int64_t)T_ * 2, st));
+  }
+  return VAP_OK;
+}
+
+
 // Back end of a clip range: downsample, transformer stack, combinator, heads.  On `st`.
 template <typename T>
 int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logits, float* vadl, float* enc_out,
@@ -710,34 +760,189 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
   for (int l = 0; l < h->dims.cross_layers; ++l)
     if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, r, st))) return rc;
 
-  // combinator (modules.py:434-449) + heads (model.py:257-261)
-  T* RAW = (T*)(ws + p.RAW) + r.s0() * t1;
-  float* HC = (float*)(ws + p.HC) + r.c0 * t1;
-  T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
+  return heads<T>(h, p, ws, r, logits, vadl, st);
+}
+
+// ------------------------------------------------------------------------ time-chunked forward
+// bf16 transformer layer on frames [f0, f1) of EVERY sequence (time-chunked back end).  The layer's
+// Q/K/V (self) and K/V (cross) live in per-layer buffers so later chunks attend to earlier ones:
+// attention is causal, so queries [f0, f1) need keys [0, f1) only (modules.py:169-202).
+int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, int li, int ci,
+                int f0, int f1, hipStream_t st) {
+  using T = bf16;
+  const int T_ = p.T, S = p.S, nf = f1 - f0;
+  const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
+  float* X = (float*)(ws + p.X);
+  T* QKV = (T*)(ws + p.QKVL) + (int64_t)li * S * t3;
+  T* KVC = (T*)(ws + p.KVCL) + (int64_t)ci * S * t2;
+  T* QC = (T*)(ws + p.QC);
+  T* ATT = (T*)(ws + p.ATT);
+  T* FF = (T*)(ws + p.FF);
+  const int H = h->dims.num_heads;
+  const float scale = 1.0f / std::sqrt((float)D);
+  // row-panel over rows (s, t in [f0, f1)); A / C point at row f0 of sequence 0
+  auto rp = [&](const void* A, int64_t lda, int64_t aseq, const std::string& w, int N, void* C, int64_t ldc,
+                int64_t cseq, const float* add, const std::string& ln, int amode, int epi) {
+    RowPanelArgs a{A, lda, S * nf, h->W<T>(w), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
+                   ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
+    a.rows_per_seq = nf;
+    a.a_seq = aseq;
+    a.c_seq = cseq;
+    return launch_rowpanel(a, amode, epi, st);
+  };
+  float* Xf = X + (int64_t)f0 * D;
   {
-    Timed tm(h, VAP_K_HEADS, st);
-    HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
-    // channel-0 rows are the even sequences: stride 2*T*D over the clips of the range
-    GemmArgs ga = gargs(RAW, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, T_, r.nc, HC, D, t1);
-    ga.norm = 2;
-    ga.act = 2;
-    ga.gamma = h->P("ar.combinator.ln.weight");
-    ga.beta = h->P("ar.combinator.ln.bias");
-    HIPCHK(gemm<T>(ga, st, true));
-    GemmArgs gb = ga;
-    gb.A = RAW + t1;
-    gb.W = h->W<T>("comb_b");
-    gb.add = HC;
-    gb.ld_add = D;
-    gb.add_seq_stride = t1;
-    HIPCHK(gemm<T>(gb, st, true));
-    HIPCHK(launch_layernorm<T>(HC, (int64_t)r.nc * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
-    HIPCHK(gemm<T>(gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
-                         logits + r.c0 * (int64_t)T_ * 256, 256, (int64_t)T_ * 256), st, true));
-    HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
-                           vadl + r.c0 * (int64_t)T_ * 2, st));
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(Xf, D, t1, pre + ".qkv", 3 * D, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_self_attn", 1, 0));
+    if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
+      HIPCHK(rp(Xf, D, t1, pre + ".kvc", 2 * D, KVC + (int64_t)f0 * 2 * D, 2 * D, t2, nullptr, "", 2, 0));
+  }
+  {
+    Timed tm(h, VAP_K_ATTN, st);
+    AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, f1, H,
+               0, scale};
+    a.q0 = f0;
+    HIPCHK(launch_attention<T>(a, st));
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".o", D, Xf, D, t1, Xf, "", 0, 2));
+  }
+  if (cross) {
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      HIPCHK(rp(Xf, D, t1, pre + ".qc", D, QC + (int64_t)f0 * D, D, t1, nullptr, pre + ".ln_src_attn", 1, 0));
+    }
+    {
+      Timed tm(h, VAP_K_ATTN, st);
+      AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, f1, H, 1,
+                 scale};
+      a.q0 = f0;
+      HIPCHK(launch_attention<T>(a, st));
+    }
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);
+      HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".oc", D, Xf, D, t1, Xf, "", 0, 2));
+    }
+  }
+  {
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(rp(Xf, D, t1, pre + ".w1", 3 * D, FF + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_ffnetwork", 1, 1));
+    GemmArgs g2 = gargs(FF + (int64_t)f0 * 3 * D, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, nf, S, Xf, D, t1);
+    g2.add = Xf;
+    g2.ld_add = D;
+    g2.add_seq_stride = t1;
+    HIPCHK(gemm<T>(g2, st, true));
   }
   return VAP_OK;
+}
+
+// VapGPT.forward pipelined ALONG TIME (bf16, 1-layer LSTM).  The frames are cut into `nch` chunks;
+// on the caller's stream the front end of chunk c computes only the conv / gate-projection rows
+// that chunk needs (receptive fields: conv4 rows [., e) need conv3 rows < 2e+1, and so on down to
+// conv1), then publishes ready[c]; one persistent LSTM launch on a side stream runs every
+// sequence's recurrence, waiting at each chunk boundary and publishing done[c]; the back end of
+// chunk c (downsample, every transformer layer on the chunk's frames -- causal, so only earlier
+// keys are needed) waits for done[c].  The serial LSTM thus overlaps the whole front end and the
+// earlier chunks' back ends, for all clips at once.
+int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, float* logits, float* vadl,
+                   unsigned char* ws, hipStream_t st) {
+  using T = bf16;
+  const int S = p.S, T_ = p.T;
+  const int64_t* L = p.L;
+  const std::string g = "encoder.encoder.gEncoder";
+  int nch = std::min(h->time_chunks, vap_handle::MAXMB);
+  nch = std::max(1, std::min(nch, T_ / 32));  // chunks of at least 32 frames
+  // frame chunks [fb[c], fb[c+1]) and LSTM step chunk ends
+  int fb[vap_handle::MAXMB + 1];
+  for (int c = 0; c <= nch; ++c) fb[c] = (int)((int64_t)T_ * c / nch);
+  LstmSync sy{};
+  sy.ready = h->sync_mem;
+  sy.done = h->sync_mem + vap_handle::MAXMB;
+  sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
+  sy.epoch = ++h->epoch;
+  sy.nr = nch;
+  sy.time_mode = 1;
+  for (int c = 0; c < nch; ++c) sy.seq_end[c] = c + 1 == nch ? (int)L[4] : std::min((int)L[4], 2 * fb[c + 1]);
+  const int nwg = (S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
+  for (int c = 0; c < nch; ++c) h->done_expect[c] += nwg;
+
+  // the recurrence: one launch, every sequence, gated by the ready flags
+  hipStream_t side = h->side[0];
+  hipEvent_t fork = h->next_fork_event();
+  HIPCHK(hipEventRecord(fork, st));
+  HIPCHK(hipStreamWaitEvent(side, fork, 0));
+  T* GX = (T*)(ws + p.GX);
+  {
+    Timed tm(h, VAP_K_LSTM_REC, side);
+    HIPCHK(launch_lstm_resident(GX, S, (int)L[4], h->W<T>("whh_l0"), (T*)(ws + p.H0) + 4 * D, p.sh, side, &sy));
+  }
+
+  // ---- front end, chunk by chunk
+  T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
+  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
+  int64_t done_rows[4] = {0, 0, 0, 0};
+  for (int c = 0; c < nch; ++c) {
+    int64_t e[4];
+    e[3] = sy.seq_end[c];
+    for (int i = 2; i >= 0; --i) e[i] = c + 1 == nch ? L[i + 1] : std::min(L[i + 1], 2 * e[i + 1] + 1);
+    if (e[0] > done_rows[0]) {
+      Timed tm(h, VAP_K_CONV1, st);
+      HIPCHK(launch_conv01(wav, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"), h->fpacked.at("conv0_stat"),
+                           h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), h->P(g + ".conv1.bias"),
+                           h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"), (bf16*)(Xs[0] + D), p.s1, st,
+                           (int)done_rows[0], (int)e[0]));
+    }
+    for (int i = 1; i < 4; ++i) {  // conv2..4: implicit GEMMs on the new rows (encoder_components.py:100-103)
+      const int64_t a = done_rows[i], b = e[i];
+      if (b <= a) continue;
+      const std::string cs = std::to_string(i + 1);
+      Timed tm(h, VAP_K_CONV234, st);
+      GemmArgs ga = gargs(Xs[i - 1] + a * 2 * D, 2 * D, ss[i - 1], h->W<T>("conv" + cs), 4 * D, D,
+                          h->P(g + ".conv" + cs + ".bias"), (int)(b - a), S, Xs[i] + D + a * D, D, ss[i]);
+      ga.norm = 1;
+      ga.act = 1;
+      ga.gamma = h->P(g + ".batchNorm" + cs + ".weight");
+      ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
+      HIPCHK(gemm<T>(ga, st, false));
+    }
+    {  // LSTM gate projection of the new steps
+      const int64_t a = done_rows[3], b = e[3];
+      Timed tm(h, VAP_K_LSTM_PROJ, st);
+      HIPCHK(gemm<T>(gargs(Xs[3] + D + a * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)(b - a),
+                           S, GX + a * 4 * D, 4 * D, L[4] * 4 * D), st, false));
+    }
+    for (int i = 0; i < 4; ++i) done_rows[i] = e[i];
+    HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
+  }
+
+  // ---- back end, chunk by chunk
+  const int64_t t1 = (int64_t)T_ * D;
+  T* Hf = (T*)(ws + p.H0);
+  float* X = (float*)(ws + p.X);
+  int rc;
+  for (int c = 0; c < nch; ++c) {
+    const int f0 = fb[c], f1 = fb[c + 1];
+    HIPCHK(hipStreamWaitValue32(st, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
+    {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
+      Timed tm(h, VAP_K_DOWNSAMPLE, st);
+      GemmArgs ga = gargs(Hf + (int64_t)f0 * 2 * D, 2 * D, p.sh, h->W<T>("down"), 5 * D, D,
+                          h->P("encoder.downsample.1.bias"), f1 - f0, S, X + (int64_t)f0 * D, D, t1);
+      ga.norm = 2;
+      ga.act = 2;
+      ga.gamma = h->P("encoder.downsample.2.ln.weight");
+      ga.beta = h->P("encoder.downsample.2.ln.bias");
+      HIPCHK(gemm<T>(ga, st, true));
+    }
+    int li = 0;
+    for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
+      if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, st))) return rc;
+    for (int l = 0; l < h->dims.cross_layers; ++l, ++li)
+      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, st))) return rc;
+  }
+  HIPCHK(hipEventRecord(h->mb_ev[0], side));  // join: the LSTM launch has fully retired
+  HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
+  return heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, st);
 }
 
 // VapGPT.forward (model.py:249-268).  Micro-batch pipeline: the batch is split into up to
@@ -748,7 +953,7 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
 template <typename T>
 int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits, float* vadl, unsigned char* ws,
                 hipStream_t st, float* enc_out = nullptr) {
-  const Plan p = make_plan(B, N, sizeof(T));
+  const Plan p = plan_for(h, B, N);
   const int S = p.S;
   const int64_t* L = p.L;
   // pad rows (conv zero padding lives in explicit rows)
@@ -776,6 +981,12 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
     if (c1 > c0) rs.push_back({c0, c1 - c0});
   }
   int rc;
+  if constexpr (sizeof(T) == 2) {
+    if (h->use_time_chunks() && !enc_out && p.QKVL) {
+      if ((rc = h->ensure_streams())) return rc;
+      if (h->wait_value) return run_forward_tc(h, p, wav, N, logits, vadl, ws, st);
+    }
+  }
   if (rs.size() == 1) {
     if ((rc = front_end<T>(h, p, wav, N, ws, rs[0], st))) return rc;
     for (int l = 0; l < NL; ++l)
@@ -868,6 +1079,8 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
   if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
+  if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
+  if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);
   for (auto& kv : h->params) {
@@ -937,7 +1150,7 @@ int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t
   int64_t L[6];
   frame_lengths(n_samples, L);
   if (L[5] <= 0) return fail(VAP_ERR_INVALID, "waveform too short for one frame");
-  *bytes = make_plan(batch, n_samples, h->dims.precision == VAP_PRECISION_BF16 ? 2 : 4).total;
+  *bytes = plan_for(h, batch, n_samples).total;
   return VAP_OK;
 }
 

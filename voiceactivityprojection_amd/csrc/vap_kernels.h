@@ -60,7 +60,10 @@ struct LstmSync {
   unsigned* error;   // set to 1 if a ready flag did not arrive within ~2 s (never expected)
   unsigned epoch;
   int nr;            // number of ranges
-  int seq_end[16];   // exclusive end sequence of each range
+  int seq_end[16];   // exclusive end sequence of each range (time_mode: exclusive end STEP of each
+                     // time chunk: every workgroup waits ready[c] before the chunk and adds 1 to
+                     // done[c] after it)
+  int time_mode;
 };
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
                                 int64_t out_seq_stride, hipStream_t st, const LstmSync* sync);
@@ -75,6 +78,8 @@ struct AttnArgs {
   int S, T, H;
   int kv_swap;                            // 0: self (K/V of s); 1: cross (K/V of s ^ 1, clip-major pairs)
   float scale;
+  int q0 = 0;                             // queries [q0, T) against keys [0, T) (time-chunked back end;
+                                          // bf16 attn3 only); Q / O still point at row 0
 };
 template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
@@ -107,7 +112,7 @@ hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, 
 // c0w: [256][32] bf16 split-bf16 conv0 operand; c0stat: centred Gram statistics (112 floats).
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
                          const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
-                         bf16* out, int64_t out_seq_stride, hipStream_t st);
+                         bf16* out, int64_t out_seq_stride, hipStream_t st, int r0 = 0, int r1 = -1);
 
 // Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
 // amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).
@@ -124,5 +129,9 @@ struct RowPanelArgs {
   const float* gamma;
   const float* beta;
   float eps;
+  // rows_per_seq > 0: row m = (s = m / rows_per_seq, t = m % rows_per_seq) at A + s*a_seq + t*lda,
+  // C / add + s*c_seq + t*ldc (a time chunk of every sequence); 0: rows contiguous
+  int rows_per_seq = 0;
+  int64_t a_seq = 0, c_seq = 0;
 };
 hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st);
