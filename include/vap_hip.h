@@ -135,6 +135,9 @@ int vap_test_layernorm(int precision, const float* x, int64_t rows, const float*
 int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
                       const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
 
+/* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
+int vap_test_read_stamps(unsigned long long* out);
+
 #ifdef __cplusplus
 }
 #endif

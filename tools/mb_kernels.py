@@ -80,7 +80,10 @@ def bench_gemm(lib, dev, st, iters, only=""):
              ("conv2_plain", 16002, 512, 1024, 256, 8000, 0, 0, 0, 0),
              ("conv3_cn_relu", 8002, 512, 1024, 256, 4000, 1, 1, 0, 0),
              ("lstm_proj", 2000, 256, 256, 1024, 2000, 0, 0, 0, 0),
-             ("ff2_resid", 1000, 768, 768, 256, 1000, 0, 0, 1, 1)]
+             ("ff2_resid", 1000, 768, 768, 256, 1000, 0, 0, 1, 1),
+             ("ksweep_k512", 16002, 512, 512, 256, 8000, 0, 0, 0, 0),
+             ("ksweep_k2048", 16002, 512, 2048, 256, 8000, 0, 0, 0, 0),
+             ("ksweep_k4096", 16002, 512, 4096, 256, 8000, 0, 0, 0, 0)]
     S = 32
     for name, rin, lda, K, N, M, norm, act, out_f32, resid in cases:
         if only and only not in name:

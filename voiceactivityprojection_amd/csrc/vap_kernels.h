@@ -113,6 +113,7 @@ hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, 
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
                          const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
                          bf16* out, int64_t out_seq_stride, hipStream_t st, int r0 = 0, int r1 = -1);
+hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CONV01_STAMPS=1)
 
 // Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
 // amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).

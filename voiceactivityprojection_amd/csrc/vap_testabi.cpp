@@ -117,4 +117,6 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
   return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
 }
 
+int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
+
 }  // extern "C"
