@@ -135,6 +135,8 @@ int vap_test_layernorm(int precision, const float* x, int64_t rows, const float*
 int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
                       const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
 
+/* fused FFN block (bf16 path): x [M][256] fp32 += W2 . GELU(W1 . LayerNorm(x)), W1 [768][256] / W2 [256][768] bf16 */
+int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
 

@@ -238,3 +238,26 @@ def test_rowpanel_rejects_bad_shapes():
     C = torch.zeros(64, 200, device="cuda", dtype=torch.bfloat16)
     rc = L.lib().vap_test_rowpanel(_p(z), 256, 64, _p(W), 256, 200, _p(C), 200, None, None, None, 2, 0, _st())
     assert rc != 0
+
+
+@pytest.mark.parametrize("M", [1, 77, 1000])
+def test_ffn_fused(M):
+    """Fused FFN block (bf16 path): x += W2 . GELU(W1 . LN(x)) with the hidden in LDS, against the
+    torch fp32 composition on the same bf16-rounded operands (the LN output and the GELU output are
+    rounded to bf16 inside the kernel, as the unfused row-panel path rounds them)."""
+    L = lib()
+    D = 256
+    g = torch.Generator().manual_seed(21 + M)
+    x = torch.randn(M, D, generator=g) * 2 + 0.3
+    ga = 1 + 0.2 * torch.randn(D, generator=g)
+    be = 0.1 * torch.randn(D, generator=g)
+    W1 = (torch.randn(3 * D, D, generator=g) / 16).to(torch.bfloat16)
+    W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16)
+    dx = x.clone().cuda()
+    d = [t.cuda() for t in (W1, W2, ga, be)]
+    _run(L.lib().vap_test_ffn, _p(dx), M, _p(d[0]), _p(d[1]), _p(d[2]), _p(d[3]), _st())
+    a = F.layer_norm(x, (D,), ga, be).to(torch.bfloat16).float()
+    hdn = F.gelu(a @ W1.float().t()).to(torch.bfloat16).float()
+    ref = x + hdn @ W2.float().t()
+    err = (dx.cpu() - ref).abs().max().item()
+    assert err <= 2e-3 * max(1.0, ref.abs().max().item()), f"ffn M={M}: {err}"

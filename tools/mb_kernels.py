@@ -116,6 +116,34 @@ def bench_gemm(lib, dev, st, iters, only=""):
     return res
 
 
+def bench_ffn(lib, dev, st, iters, M):
+    """Fused FFN block vs the unfused row-panel up + GEMM down, at one layer-chunk (M rows)."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    D = 256
+    x0 = torch.randn(M, D, generator=g).to(dev)
+    x = x0.clone()
+    ga = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    be = (0.1 * torch.randn(D, generator=g)).to(dev)
+    W1 = (torch.randn(3 * D, D, generator=g) / 16).to(torch.bfloat16).to(dev)
+    W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16).to(dev)
+    FF = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+
+    def fused():
+        _native.check(lib.vap_test_ffn(ptr(x), M, ptr(W1), ptr(W2), ptr(ga), ptr(be), st))
+
+    def unfused():
+        _native.check(lib.vap_test_rowpanel(ptr(x), D, M, ptr(W1), D, 3 * D, ptr(FF), 3 * D, None, ptr(ga), ptr(be),
+                                            1, 1, st))
+        _native.check(lib.vap_test_gemm(1, ptr(FF), 3 * D, M * 3 * D, ptr(W2), 3 * D, D, None, M, 1, ptr(x), D, M * D,
+                                        ptr(x), D, M * D, None, None, 0, 0, 1, st))
+    res = {}
+    for name, fn in [("ffn_fused", fused), ("ffn_unfused", unfused)]:
+        us = timeit(fn, iters)
+        res[name] = dict(us=round(us, 2), tflops=round(2.0 * M * 2 * 3 * D * D / us / 1e6, 1))
+        print(name, res[name], flush=True)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32000)
@@ -135,6 +163,8 @@ def main():
     res = {}
     if "attn" in args.which:
         res.update(bench_attn(lib, dev, st, args.iters))
+    if "ffn" in args.which:
+        res.update(bench_ffn(lib, dev, st, args.iters, args.rows))
     if "gemm" in args.which:
         res.update(bench_gemm(lib, dev, st, args.iters, args.case))
     if "rowpanel" not in args.which:

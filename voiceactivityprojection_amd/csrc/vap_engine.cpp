@@ -52,6 +52,8 @@ struct vap_handle {
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
   bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
+  bool ffn_fused = false;  // VAP_FFN_FUSED=1: bf16 FFN with the hidden in LDS (k_ffn.hip; one workgroup per CU:
+                           // measured 113 us vs 84 us unfused per 32k rows -- kept as an option)
   hipStream_t side[NSIDE] = {};
   hipEvent_t mb_ev[MAXMB] = {};
   hipEvent_t fork_ev[MAXMB] = {};
@@ -65,6 +67,7 @@ struct vap_handle {
   bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
   bool persistent_lstm = true;  // VAP_PERSISTENT_LSTM=0: one LSTM launch per range on the side streams
   int time_chunks = 4;          // VAP_TIME_CHUNKS (bf16, 1-layer LSTM): pipeline the forward along time
+  int tc_streams = 1;           // VAP_TC_STREAMS=2: back ends on their own stream (measured: no gain, kernels fill the GPU)
   bool use_time_chunks() const {
     return dims.precision == VAP_PRECISION_BF16 && dims.lstm_layers == 1 && time_chunks >= 2;
   }
@@ -518,12 +521,18 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(X, D, pre + ".w1", 3 * D, FF, 3 * D, nullptr, pre + ".ln_ffnetwork", 1, 1));
-    GemmArgs g2 = gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1);
-    g2.add = X;
-    g2.ld_add = D;
-    g2.add_seq_stride = t1;
-    HIPCHK(gemm<T>(g2, st, true));
+    if (h->ffn_fused) {
+      FfnArgs f{X, rows, 0, 0, h->W<T>(pre + ".w1"), h->W<T>(pre + ".w2"), h->P(pre + ".ln_ffnetwork.weight"),
+                h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+      HIPCHK(launch_ffn(f, st));
+    } else {
+      HIPCHK(rp(X, D, pre + ".w1", 3 * D, FF, 3 * D, nullptr, pre + ".ln_ffnetwork", 1, 1));
+      GemmArgs g2 = gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1);
+      g2.add = X;
+      g2.ld_add = D;
+      g2.add_seq_stride = t1;
+      HIPCHK(gemm<T>(g2, st, true));
+    }
   }
   return VAP_OK;
 }
@@ -827,12 +836,18 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(Xf, D, t1, pre + ".w1", 3 * D, FF + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_ffnetwork", 1, 1));
-    GemmArgs g2 = gargs(FF + (int64_t)f0 * 3 * D, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, nf, S, Xf, D, t1);
-    g2.add = Xf;
-    g2.ld_add = D;
-    g2.add_seq_stride = t1;
-    HIPCHK(gemm<T>(g2, st, true));
+    if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
+      FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1"), h->W<T>(pre + ".w2"), h->P(pre + ".ln_ffnetwork.weight"),
+                h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+      HIPCHK(launch_ffn(f, st));
+    } else {
+      HIPCHK(rp(Xf, D, t1, pre + ".w1", 3 * D, FF + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_ffnetwork", 1, 1));
+      GemmArgs g2 = gargs(FF + (int64_t)f0 * 3 * D, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, nf, S, Xf, D, t1);
+      g2.add = Xf;
+      g2.ld_add = D;
+      g2.add_seq_stride = t1;
+      HIPCHK(gemm<T>(g2, st, true));
+    }
   }
   return VAP_OK;
 }
@@ -916,33 +931,46 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
     HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
   }
 
-  // ---- back end, chunk by chunk
+  // ---- back end, chunk by chunk: on its own stream (bst) so that chunk c's transformer overlaps
+  // the front ends of the later chunks (the kernels of either side leave CUs / pipes idle in their
+  // prologues, epilogues and phase barriers); the LSTM hand-off orders them
   const int64_t t1 = (int64_t)T_ * D;
   T* Hf = (T*)(ws + p.H0);
   float* X = (float*)(ws + p.X);
+  hipStream_t bst = h->tc_streams >= 2 ? h->side[1] : st;
+  if (bst != st) {
+    hipEvent_t fk = h->next_fork_event();  // the back-end stream starts after this call's set-up
+    HIPCHK(hipEventRecord(fk, st));
+    HIPCHK(hipStreamWaitEvent(bst, fk, 0));
+  }
   int rc;
   for (int c = 0; c < nch; ++c) {
     const int f0 = fb[c], f1 = fb[c + 1];
-    HIPCHK(hipStreamWaitValue32(st, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
+    HIPCHK(hipStreamWaitValue32(bst, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
     {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
-      Timed tm(h, VAP_K_DOWNSAMPLE, st);
+      Timed tm(h, VAP_K_DOWNSAMPLE, bst);
       GemmArgs ga = gargs(Hf + (int64_t)f0 * 2 * D, 2 * D, p.sh, h->W<T>("down"), 5 * D, D,
                           h->P("encoder.downsample.1.bias"), f1 - f0, S, X + (int64_t)f0 * D, D, t1);
       ga.norm = 2;
       ga.act = 2;
       ga.gamma = h->P("encoder.downsample.2.ln.weight");
       ga.beta = h->P("encoder.downsample.2.ln.bias");
-      HIPCHK(gemm<T>(ga, st, true));
+      HIPCHK(gemm<T>(ga, bst, true));
     }
     int li = 0;
     for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
-      if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, st))) return rc;
+      if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, bst))) return rc;
     for (int l = 0; l < h->dims.cross_layers; ++l, ++li)
-      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, st))) return rc;
+      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst))) return rc;
   }
+  if ((rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst))) return rc;
   HIPCHK(hipEventRecord(h->mb_ev[0], side));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
-  return heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, st);
+  if (bst != st) {
+    HIPCHK(hipEventRecord(h->mb_ev[1], bst));
+    HIPCHK(hipStreamWaitEvent(st, h->mb_ev[1], 0));
+  }
+  return VAP_OK;
 }
 
 // VapGPT.forward (model.py:249-268).  Micro-batch pipeline: the batch is split into up to
@@ -1078,8 +1106,10 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
   if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
+  if (const char* e = getenv("VAP_FFN_FUSED")) h->ffn_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
+  if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);
   if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);

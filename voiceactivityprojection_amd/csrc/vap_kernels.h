@@ -136,3 +136,18 @@ struct RowPanelArgs {
   int64_t a_seq = 0, c_seq = 0;
 };
 hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st);
+
+// Fused FFN block (k_ffn.hip, bf16): x += W2 . GELU(W1 . LayerNorm(x)), x fp32 [rows][256] in place,
+// W1 [768][256], W2 [256][768] bf16.  Row addressing as RowPanelArgs (rows_per_seq / x_seq).
+struct FfnArgs {
+  float* x;
+  int M;
+  int rows_per_seq;  // 0: rows contiguous (stride 256)
+  int64_t x_seq;
+  const void* W1;
+  const void* W2;
+  const float* gamma;
+  const float* beta;
+  float eps;
+};
+hipError_t launch_ffn(const FfnArgs& g, hipStream_t st);

@@ -117,6 +117,11 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
   return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
 }
 
+int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream) {
+  FfnArgs g{x, M, 0, 0, W1, W2, gamma, beta, 1e-5f};
+  return rc_of(launch_ffn(g, (hipStream_t)stream));
+}
+
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
 
 }  // extern "C"
