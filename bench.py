@@ -54,7 +54,7 @@ def class_flops(B: int, n: int, heads: int = 4, channel_layers: int = 1, cross_l
     return f, L
 
 
-def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int = 4):
+def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int = 32):
     """Time the CPU oracle (torch fp32 restatement of the reference) on a bounded sample."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import vap_oracle as O
@@ -180,6 +180,16 @@ def main():
         flop_per_launch = flops[dominant] / launches_per_step
         achieved = flop_per_launch / (dom_ms_per_launch * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
+        # HBM traffic of the dominant kernel: PMC-measured bytes per output row (profiles/, collected
+        # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
+        # by the concurrent LSTM) x the rows of one launch here
+        traffic, traffic_src = None, None
+        tp = os.path.join(REPO, "profiles", "r1_traffic_pmc.json")
+        if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
+            per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
+            rows_per_launch = 2 * B * L[1] / launches_per_step
+            traffic = round(per_row * rows_per_launch / 1e9, 3)
+            traffic_src = "profiles/r1_traffic_pmc.json (GB per launch)"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "audio-s/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
@@ -190,7 +200,8 @@ def main():
                        "parallelism": f"dp{world}", "step": "VapGPT.probs (forward + probs epilogue + labels/loss)"
                                                             + (" + RCCL gather to rank 0" if dist else "")},
             "roofline": {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "flop_per_launch": flop_per_launch, "ms_per_launch": round(dom_ms_per_launch, 4),
                          "launches": cnt.value},
             "breakdown_ms_per_step": breakdown,

@@ -537,15 +537,21 @@ __global__ __launch_bounds__(512, 1) void conv01b_kernel(const float* __restrict
     rstd[i] = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
   }
   bf16* obase = out + (int64_t)s * out_seq_stride;
+  // rows outer, column tiles inner: a wave completes each 128-B line of a row in consecutive stores
+  // (column-outer order wrote ~1.9x the output bytes to HBM: partial lines left L2 between stores)
+  f32x4 ga[4], be[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const f32x4 ga = *(const f32x4*)(g1 + nb + j * 16);
-    const f32x4 be = *(const f32x4*)(be1 + nb + j * 16);
+    ga[j] = *(const f32x4*)(g1 + nb + j * 16);
+    be[j] = *(const f32x4*)(be1 + nb + j * 16);
+  }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = t0 + wm * 64 + i * 16 + (lane & 15);
-      if (t >= r1) continue;
-      f32x4 v = (acc[j][i] - mean[i]) * rstd[i] * ga + be;
+  for (int i = 0; i < 4; ++i) {
+    const int t = t0 + wm * 64 + i * 16 + (lane & 15);
+    if (t >= r1) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 v = (acc[j][i] - mean[i]) * rstd[i] * ga[j] + be[j];
       store4(obase + (int64_t)t * BN + nb + j * 16, fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f),
              fmaxf(v[3], 0.f));
     }
