@@ -131,7 +131,8 @@ int vap_test_probe_mfma_f32(const float* a, const float* b, float* d, void* stre
 int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
                        void* raw, void* stream);
 /* row-panel projection GEMM (bf16 perf path, K = 256): amode 0 bf16 A / 1 fp32 A + LayerNorm /
- * 2 fp32 A raw; epi 0 bf16 out / 1 GELU bf16 out / 2 fp32 out + residual `add` (ld = ldc). */
+ * 2 fp32 A raw; epi 0 bf16 out / 1 GELU bf16 out / 2 fp32 out + residual `add` (ld = ldc).
+ * amode | 16: W is given in the packed row-panel layout [N/256][K/32][16][64][8]. */
 int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
                       const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
 
@@ -139,6 +140,8 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
 int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
+/* timing diagnostics: 8 x 32 s_memtime stamps of sampled row-panel workgroups (VAP_RP_STAMPS=1) */
+int vap_test_read_rp_stamps(unsigned long long* out);
 
 #ifdef __cplusplus
 }

@@ -203,9 +203,10 @@ def test_layernorm(prec):
 
 @pytest.mark.parametrize("amode,epi,N", [(1, 0, 768), (1, 0, 256), (1, 1, 768), (2, 0, 512), (0, 2, 256)])
 @pytest.mark.parametrize("M", [1, 77, 1000])
-def test_rowpanel(amode, epi, N, M):
+@pytest.mark.parametrize("packed", [0, 1])
+def test_rowpanel(amode, epi, N, M, packed):
     """Row-panel projection GEMM (bf16 perf path): LN / raw fp32 / bf16 A panel, bf16 / GELU /
-    fp32+residual epilogue, ragged last panel."""
+    fp32+residual epilogue, ragged last panel; W in the plain or the packed row-panel layout."""
     L = lib()
     D = 256
     g = torch.Generator().manual_seed(11 + M + N)
@@ -218,8 +219,10 @@ def test_rowpanel(amode, epi, N, M):
     dA, dW, dga, dbe = A.cuda(), W.cuda(), ga.cuda(), be.cuda()
     dadd = add.cuda() if add is not None else None
     C = torch.zeros(M, N, device="cuda", dtype=torch.float32 if epi == 2 else torch.bfloat16)
+    if packed:  # [N/256][K/32][16 row groups][64 lanes][8]: lane = (k%32)/8*16 + n%16
+        dW = dW.view(N // 256, 16, 16, 8, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
     _run(L.lib().vap_test_rowpanel, _p(dA), D, M, _p(dW), D, N, _p(C), N, _p(dadd),
-         _p(dga) if amode == 1 else None, _p(dbe) if amode == 1 else None, amode, epi, _st())
+         _p(dga) if amode == 1 else None, _p(dbe) if amode == 1 else None, amode | (16 * packed), epi, _st())
     a = F.layer_norm(x, (D,), ga, be) if amode == 1 else x
     ref = a.to(torch.bfloat16).float() @ W.float().t()
     if epi == 1:

@@ -144,12 +144,19 @@ def bench_ffn(lib, dev, st, iters, M):
     return res
 
 
+def pack_rowpanel(W):
+    """[N][256] bf16 -> the packed row-panel layout [N/256][8][16][64][8] (lane = (k%32)/8*16 + n%16)."""
+    N = W.shape[0]
+    return W.view(N // 256, 16, 16, 8, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32000)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--which", default="rowpanel,attn")
     ap.add_argument("--case", default="", help="only GEMM cases whose name contains this")
+    ap.add_argument("--packed", action="store_true", help="row-panel W in the packed layout")
     args = ap.parse_args()
     lib = _native.lib()
     dev = torch.device("cuda:0")
@@ -177,10 +184,13 @@ def main():
         add = torch.randn(M, N, generator=g).to(dev) if epi == 2 else None
         C = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == 2 else torch.bfloat16)
 
+        Wk = pack_rowpanel(W) if args.packed else W
+
         def run():
-            _native.check(lib.vap_test_rowpanel(ptr(A), D, M, ptr(W), D, N, ptr(C), N, ptr(add),
+            _native.check(lib.vap_test_rowpanel(ptr(A), D, M, ptr(Wk), D, N, ptr(C), N, ptr(add),
                                                 ptr(gamma) if amode == 1 else None,
-                                                ptr(beta) if amode == 1 else None, amode, epi, st))
+                                                ptr(beta) if amode == 1 else None,
+                                                amode | (16 if args.packed else 0), epi, st))
         us = timeit(run, args.iters)
         # check against torch (fp32 math on the bf16-rounded operands)
         a = x

@@ -63,6 +63,7 @@ _SIGS = {
     "vap_test_conv0": (ctypes.c_int, [ctypes.c_int, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "vap_test_layernorm": (ctypes.c_int, [ctypes.c_int, _P, _I64, _P, _P, _P, _P, _P]),
     "vap_test_read_stamps": (ctypes.c_int, [_P]),
+    "vap_test_read_rp_stamps": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_rowpanel": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _I64,
                                          _P, _P, _P, ctypes.c_int, ctypes.c_int, _P]),

@@ -86,3 +86,33 @@ VAP_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
 VAP_DEV chunk16 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(chunk16, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
+
+// Range-checked buffer stores: a lane whose offset lies outside the resource writes nothing, so
+// bounds are handled without branches (conditional stores also defeat the compiler's vmcnt
+// bookkeeping for the loads issued after them).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+VAP_DEV void buf_store8(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)voff, 0, 0);
+}
+VAP_DEV void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, 0);
+}
+VAP_DEV u32x2 pack_bf16x4(float a, float b, float c, float d) {
+  const bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return __builtin_bit_cast(u32x2, v);
+}
+
+// GELU(x) = x * Phi(x) with Phi from the erfc approximation of Abramowitz & Stegun 7.1.26
+// (|erf error| <= 1.5e-7, i.e. |GELU error| <= 7.5e-8 |x|): one v_rcp, one v_exp and ~10 FMAs
+// instead of the ~50-instruction erff.  Used where the result is rounded to bf16.
+VAP_DEV float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float h = 0.5f * p * t * __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);  // erfc(z) / 2
+  return x * (x >= 0.f ? 1.0f - h : h);
+}

@@ -430,16 +430,28 @@ int pack_all(vap_handle* h, hipStream_t st) {
     }
     return VAP_OK;
   };
+  // bf16: the row-panel projections (K = 256) also get a copy in the packed row-panel layout,
+  // "<name>@rp" (one k-step tile 16 KiB contiguous, one wave fragment 1 KiB: k_rowpanel.hip)
+  auto rp_copy = [&](const std::string& name, int N) -> int {
+    if constexpr (sizeof(T) == 2) {
+      T* w = alloc(name + "@rp", (int64_t)N * D);
+      if (!w) return fail(VAP_ERR_HIP, "hipMalloc " + name + "@rp");
+      HIPCHK(launch_pack_rowpanel((const bf16*)h->packed.at(name), (bf16*)w, N, st));
+    }
+    return VAP_OK;
+  };
   auto layer = [&](const std::string& p, bool cross) -> int {
     int rc;
     if ((rc = cat(p + ".qkv", {p + ".mha.query.weight", p + ".mha.key.weight", p + ".mha.value.weight"}))) return rc;
     if ((rc = cat(p + ".o", {p + ".mha.proj.weight"}))) return rc;
     if ((rc = cat(p + ".w1", {p + ".ffnetwork.0.weight"}))) return rc;
     if ((rc = cat(p + ".w2", {p + ".ffnetwork.3.weight"}))) return rc;
+    if ((rc = rp_copy(p + ".qkv", 3 * D)) || (rc = rp_copy(p + ".o", D)) || (rc = rp_copy(p + ".w1", 3 * D))) return rc;
     if (cross) {
       if ((rc = cat(p + ".qc", {p + ".mha_cross.query.weight"}))) return rc;
       if ((rc = cat(p + ".kvc", {p + ".mha_cross.key.weight", p + ".mha_cross.value.weight"}))) return rc;
       if ((rc = cat(p + ".oc", {p + ".mha_cross.proj.weight"}))) return rc;
+      if ((rc = rp_copy(p + ".qc", D)) || (rc = rp_copy(p + ".kvc", 2 * D)) || (rc = rp_copy(p + ".oc", D))) return rc;
     }
     return VAP_OK;
   };
@@ -483,8 +495,9 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
   auto rp = [&](const void* A, int64_t lda, const std::string& w, int N, void* C, int64_t ldc, const float* add,
                 const std::string& ln, int amode, int epi) {
-    RowPanelArgs a{A, lda, rows, h->W<T>(w), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
+    RowPanelArgs a{A, lda, rows, h->W<T>(w + "@rp"), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
                    ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
+    a.w_packed = 1;
     return launch_rowpanel(a, amode, epi, st);
   };
   {
@@ -792,8 +805,9 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   // row-panel over rows (s, t in [f0, f1)); A / C point at row f0 of sequence 0
   auto rp = [&](const void* A, int64_t lda, int64_t aseq, const std::string& w, int N, void* C, int64_t ldc,
                 int64_t cseq, const float* add, const std::string& ln, int amode, int epi) {
-    RowPanelArgs a{A, lda, S * nf, h->W<T>(w), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
+    RowPanelArgs a{A, lda, S * nf, h->W<T>(w + "@rp"), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
                    ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
+    a.w_packed = 1;
     a.rows_per_seq = nf;
     a.a_seq = aseq;
     a.c_seq = cseq;

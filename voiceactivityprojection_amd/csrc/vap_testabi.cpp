@@ -113,6 +113,8 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
   RowPanelArgs g{};
   g.A = A; g.lda = lda; g.M = M; g.W = W; g.K = K; g.N = N; g.C = C; g.ldc = ldc;
   g.add = add; g.gamma = gamma; g.beta = beta; g.eps = 1e-5f;
+  g.w_packed = (amode & 16) != 0;  // W already in the packed row-panel layout
+  amode &= 15;
   if ((amode == 1) != (gamma != nullptr && beta != nullptr) || (epi == 2) != (add != nullptr)) return VAP_ERR_INVALID;
   return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
 }
@@ -123,5 +125,6 @@ int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* g
 }
 
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
+int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 
 }  // extern "C"
