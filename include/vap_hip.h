@@ -137,11 +137,19 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
                       const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
 
 /* fused FFN block (bf16 path): x [M][256] fp32 += W2 . GELU(W1 . LayerNorm(x)), W1 [768][256] / W2 [256][768] bf16 */
+/* weight packing into the projection layout [N/256][K/32][16][64][8] (N % 256 == 0, K % 32 == 0) */
+int vap_test_pack_weight(const void* W, void* out, int N, int K, void* stream);
+/* fused FFN block with W1 / W2 already packed (vap_test_pack_weight) */
+int vap_test_ffn_packed(float* x, int M, const void* W1p, const void* W2p, const float* gamma, const float* beta,
+                        void* stream);
 int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 32 s_memtime stamps of sampled row-panel workgroups (VAP_RP_STAMPS=1) */
 int vap_test_read_rp_stamps(unsigned long long* out);
+/* timing diagnostics (VAP_FFN_STAMPS=1): 8 x 24 s_memtime stamps of sampled fused-FFN workgroups, then
+ * 1024 x 2 s_memrealtime start / end of every workgroup (out holds 2240 values) */
+int vap_test_read_ffn_stamps(unsigned long long* out);
 
 #ifdef __cplusplus
 }

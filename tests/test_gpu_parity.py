@@ -206,3 +206,34 @@ def test_encoder_bf16_vs_reference(m16, golden):
     for got, exp in ((x1, g["enc1"]), (x2, g["enc2"])):
         err = (got.cpu().numpy() - exp).__abs__().max()
         assert err < 0.08, f"bf16 encoder max abs err {err}"
+
+
+def test_long_60s_bf16(m16, golden):
+    """BASELINE configs[3] clip length (60 s, T = 3000) through the bf16 time-pipelined path."""
+    g = golden("long_60s")
+    w = synthetic_waveform(int(g["clip_start"]), int(g["n_samples"]))[None]
+    out = m16.probs(torch.from_numpy(w).cuda())
+    errs = _cmp(out, g, BF16_TOL)
+    print("bf16 60 s max abs err:", errs)
+
+
+def test_bench_shape_bf16(m16, m32):
+    """The bench workload itself (BASELINE configs[1]: 64 x 20 s, bf16): size-independent checks at
+    full size -- every sampled clip is bit-identical to that clip run alone (the time-chunked,
+    multi-workgroup schedule does not leak across clips) and within the bf16 tolerance of the fp32
+    parity mode on the same clip."""
+    from voiceactivityprojection_amd.weights import synthetic_batch
+
+    w = torch.from_numpy(synthetic_batch(0, 64, 320000)).cuda()
+    full = m16.probs(w)
+    assert full["probs"].shape == (64, 1000, 256)
+    for i in (0, 37, 63):
+        one = m16.probs(w[i:i + 1])
+        for k in full:
+            assert torch.equal(full[k][i:i + 1], one[k]), f"bf16 batch dependence in {k} (clip {i})"
+        ref = m32.probs(w[i:i + 1])
+        for k in ("p_now", "p_future", "vad"):
+            err = (full[k][i:i + 1] - ref[k]).abs().max().item()
+            assert err <= BF16_TOL[k], (k, i, err)
+    for k in ("probs", "p_now", "p_future", "vad", "H", "loss"):
+        assert torch.isfinite(full[k]).all(), k

@@ -128,8 +128,12 @@ def bench_ffn(lib, dev, st, iters, M):
     W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16).to(dev)
     FF = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
 
+    W1p, W2p = torch.empty_like(W1), torch.empty_like(W2)
+    _native.check(lib.vap_test_pack_weight(ptr(W1), ptr(W1p), 3 * D, D, st))
+    _native.check(lib.vap_test_pack_weight(ptr(W2), ptr(W2p), D, 3 * D, st))
+
     def fused():
-        _native.check(lib.vap_test_ffn(ptr(x), M, ptr(W1), ptr(W2), ptr(ga), ptr(be), st))
+        _native.check(lib.vap_test_ffn_packed(ptr(x), M, ptr(W1p), ptr(W2p), ptr(ga), ptr(be), st))
 
     def unfused():
         _native.check(lib.vap_test_rowpanel(ptr(x), D, M, ptr(W1), D, 3 * D, ptr(FF), 3 * D, None, ptr(ga), ptr(be),

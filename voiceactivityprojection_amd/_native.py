@@ -64,7 +64,10 @@ _SIGS = {
     "vap_test_layernorm": (ctypes.c_int, [ctypes.c_int, _P, _I64, _P, _P, _P, _P, _P]),
     "vap_test_read_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_rp_stamps": (ctypes.c_int, [_P]),
+    "vap_test_read_ffn_stamps": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
+    "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
+    "vap_test_ffn_packed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_rowpanel": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _I64,
                                          _P, _P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_probe_mfma_f32": (ctypes.c_int, [_P, _P, _P, _P]),

@@ -2,82 +2,88 @@
 //
 //   x += W2 . GELU(W1 . LayerNorm(x))          (modules.py:9-21 ffn_block, TransformerLayer :273-275)
 //
-// per 64-row panel, with the 768-wide hidden activation kept in LDS: the LayerNorm'd panel
-// (32 KiB bf16) and the GELU'd hidden (64 x 768 bf16 = 96 KiB) never touch HBM, where the
-// unfused pair wrote and re-read 2 x 49 MB per 32k rows.  W1 [768][256] and then W2 [256][768] stream
-// through one register-prefetched, double-buffered LDS stage ring (256 rows x 32 k, 32 KiB): 24
-// k-steps of the up-projection (3 N tiles of 256) followed by 24 k-steps of the down-projection.
-// Operands are swapped (C^T = W . A^T) so a lane owns 4 consecutive columns of a row: 8-byte bf16
-// writes into the hidden image, 16-byte residual reads / fp32 stores.
-// LDS 160 KiB -> one workgroup (4 waves, one per SIMD) per CU.
+// per 64-row panel with the 768-wide hidden activation kept in LDS: the LayerNorm'd panel (32 KiB
+// bf16) and the GELU'd hidden (64 x 768 bf16 = 96 KiB) never touch HBM, where the unfused pair
+// (row-panel FFN-up + GEMM FFN-down) wrote and re-read 2 x 49 MB per 32k rows and read x twice.
+//
+// One workgroup of 8 waves (two per SIMD) per CU.  Both GEMMs take their weight operand straight
+// from L2 into registers in the packed projection layout (k_misc.hip pack_rowpanel: one wave's
+// 16-row fragment of a 32-deep k-step is 1 KiB contiguous), so the only LDS traffic is the
+// activation operand and no k-loop needs a barrier:
+//   FFN-up   (K 256, N 768): wave w owns hidden columns w*96 .. +95 (6 fragments x 4 row tiles),
+//            8 k-steps, W1 fragments prefetched 2 steps ahead;  GELU -> bf16 -> hidden image.
+//   FFN-down (K 768, N 256): wave w owns output columns w*32 .. +31 (2 fragments x 4 row tiles),
+//            24 k-steps, W2 prefetched 4 steps ahead, hidden fragments double-buffered in
+//            registers; the residual rows are prefetched when the loop starts.
+// Every wave reads a distinct slice of W1 and W2, so each workgroup streams each weight once.
+// Operands are swapped (C^T = W . A^T): a lane owns 4 consecutive columns of one row.
+#include <cstdlib>
+
 #include "vap_common.h"
 #include "vap_kernels.h"
 
 namespace {
 
 constexpr int BM = 64, D = 256, DF = 768;
-constexpr int PROWB = D * 2;    // LN panel row: 512 B
-constexpr int HROWB = DF * 2;   // hidden row: 1536 B
-constexpr int BK = 32, WROWB = BK * 2;
+constexpr int PROWB = D * 2;                  // LN panel row: 512 B (32 chunks)
+constexpr int HROWB = DF * 2;                 // hidden row: 1536 B (96 chunks)
 constexpr int OFF_H = BM * PROWB;             // 32 KiB
-constexpr int OFF_W = OFF_H + BM * HROWB;     // + 96 KiB
-constexpr int LDS_BYTES = OFF_W + 2 * D * WROWB;  // + 32 KiB = 160 KiB
-constexpr int NQ1 = (DF / D) * (D / BK);      // 24 up-projection k-steps
-constexpr int NQ = NQ1 + DF / BK;             // + 24 down-projection k-steps
-constexpr int NPF = 4;
+constexpr int LDS_BYTES = OFF_H + BM * HROWB;  // + 96 KiB = 128 KiB
+constexpr int NF1 = 6, NF2 = 2;               // weight fragments per wave: up / down
+constexpr int KS1 = D / 32, KS2 = DF / 32;    // k-steps: 8 / 24
+constexpr int NPF1 = 2, NPF2 = 4;             // weight prefetch depth (k-steps)
 
-VAP_DEV int pswz(int row, int c16) { return c16 ^ (row & 15); }              // 32 chunks per panel row
-VAP_DEV int hswz(int row, int c16) { return c16 ^ (row & 15); }              // 96 chunks per hidden row
-VAP_DEV int wswz(int row, int c) { return c ^ ((row >> 2) & 2); }            // 4 chunks per W row
+// 16-B chunk c of row `row`: XOR with row%16 spreads the 16 rows of an MFMA fragment read over
+// 16 distinct bank groups (rows are 512 / 1536 B = 0 mod 256 B apart)
+VAP_DEV int xswz(int row, int c) { return c ^ (row & 15); }
 
-__global__ __launch_bounds__(256, 1) void ffn_kernel(FfnArgs g) {
+// diagnostics (VAP_FFN_STAMPS=1): wave 0 of workgroups 0, 64, .., 448 records s_memtime at [0] start,
+// [1] LN panel written, [2] after the barrier, [3 + ks] FFN-up k-step ks (8), [11] up done, [12] GELU
+// written, [13] after the barrier, [14 + ks/4] FFN-down k-steps 0, 4, .., 20, [20] stores issued,
+// [21] stores done; [22] / [23] s_memrealtime (100 MHz) at start / end
+__device__ unsigned long long g_ffn_stamps[8][24];
+__device__ unsigned long long g_ffn_wall[1024][2];  // every workgroup < 1024: realtime start / end
+
+template <bool ST>
+__global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   unsigned char* P = smem;
   unsigned char* Hh = smem + OFF_H;
-  unsigned char* Wt = smem + OFF_W;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int m0 = blockIdx.x * BM;
   const bf16* __restrict__ W1 = (const bf16*)g.W1;
   const bf16* __restrict__ W2 = (const bf16*)g.W2;
+  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && tid == 0) ? (int)(blockIdx.x >> 6) : -1;
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (samp >= 0) g_ffn_stamps[samp][k] = t;
+    }
+  };
+  stamp(0);
+  if constexpr (ST) {
+    if (samp >= 0) g_ffn_stamps[samp][22] = __builtin_amdgcn_s_memrealtime();  // 100 MHz wall clock
+    if (tid == 0 && blockIdx.x < 1024) g_ffn_wall[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+  }
   auto xoff = [&](int m) -> int64_t {  // element offset of row m of x
     if (g.rows_per_seq == 0) return (int64_t)m * D;
     const int sq = m / g.rows_per_seq;
     return (int64_t)sq * g.x_seq + (int64_t)(m - sq * g.rows_per_seq) * D;
   };
 
-  // W stream: k-step q < 24: W1 rows nt*256 + row, k = kq*32; q >= 24: W2 rows row, k = (q-24)*32
-  chunk16 rb[NPF][4];
-  auto gload = [&](int q, chunk16* r) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + i * 256, row = id >> 2, c = id & 3;
-      const bf16* src = q < NQ1 ? W1 + (int64_t)((q >> 3) * D + row) * D + (q & 7) * BK + c * 8
-                                : W2 + (int64_t)row * DF + (q - NQ1) * BK + c * 8;
-      r[i] = *(const chunk16*)src;
-    }
-  };
-  auto lstore = [&](int buf, const chunk16* r) {
-    unsigned char* base = Wt + buf * D * WROWB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + i * 256, row = id >> 2, c = id & 3;
-      *(chunk16*)(base + row * WROWB + wswz(row, c) * 16) = r[i];
-    }
-  };
-#pragma unroll
-  for (int p = 0; p < NPF; ++p) gload(p, rb[p]);
-
   // ------------------------------------------------------------ LayerNorm(x) panel -> LDS (bf16)
-  // (the coalesced fp32 row load of k_rowpanel.hip: 16 lanes read 256 contiguous bytes of a row)
+  // wave w: rows w*8 .. w*8+7 as 2 sets of 4; a 16-lane group reads 256 contiguous bytes of its row
+  // per load.  Loads are unconditional (clamped row + select): a load under a branch gets its own
+  // s_waitcnt and serialises the panel.
   {
     const int r4 = lane >> 4, cc = lane & 15;
-    f32x4 v[4][4];
+    f32x4 v[2][4];
 #pragma unroll
-    for (int set = 0; set < 4; ++set) {
-      const int m = m0 + w * 16 + set * 4 + r4;
-      const float* src = g.x + xoff(m < g.M ? m : 0) + cc * 4;
+    for (int set = 0; set < 2; ++set) {
+      const int m = m0 + w * 8 + set * 4 + r4;
+      const float* src = g.x + xoff(m < g.M ? m : g.M - 1) + cc * 4;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) v[set][jj] = m < g.M ? *(const f32x4*)(src + jj * 64) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jj = 0; jj < 4; ++jj) v[set][jj] = *(const f32x4*)(src + jj * 64);
     }
     f32x4 ga[4], be[4];
 #pragma unroll
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(256, 1) void ffn_kernel(FfnArgs g) {
       be[jj] = *(const f32x4*)(g.beta + jj * 64 + cc * 4);
     }
 #pragma unroll
-    for (int set = 0; set < 4; ++set) {
+    for (int set = 0; set < 2; ++set) {
       float sum = 0.f;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) sum += v[set][jj][0] + v[set][jj][1] + v[set][jj][2] + v[set][jj][3];
@@ -103,92 +109,165 @@ __global__ __launch_bounds__(256, 1) void ffn_kernel(FfnArgs g) {
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o, 64);
       const float rstd = rsqrtf(ss * (1.0f / D) + g.eps);
-      const int row = w * 16 + set * 4 + r4;
+      const int row = w * 8 + set * 4 + r4;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
+      for (int jj = 0; jj < 4; ++jj) {  // rows >= M hold LN(row M-1): computed, never stored
         const f32x4 y = v[set][jj] * rstd * ga[jj] + be[jj];
         const bf16x4 b = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
-        *(bf16x4*)(P + row * PROWB + pswz(row, jj * 8 + (cc >> 1)) * 16 + (cc & 1) * 8) = b;
+        *(bf16x4*)(P + row * PROWB + xswz(row, jj * 8 + (cc >> 1)) * 16 + (cc & 1) * 8) = b;
       }
     }
   }
-  lstore(0, rb[0]);
-  __syncthreads();
 
-  // ------------------------------------------------------------ 48 k-steps: 3 x 8 up, 24 down
-  f32x4 acc[4][4];  // [n tile 16 of the wave's 64 columns][m tile 16] of C^T
-  for (int q0 = 0; q0 < NQ; q0 += NPF) {
+  // ------------------------------------------------------------ FFN-up: 8 k-steps, N 768
+  // fragment i of wave w = hidden rows of W1 (w*6 + i)*16 .. +15 = row group (w*6+i) of the packed
+  // layout: N tile (w*6+i)/16, group (w*6+i)%16
+  auto w1load = [&](int ks, chunk16* r) {
 #pragma unroll
-    for (int p = 0; p < NPF; ++p) {
-      const int q = q0 + p;
-      const bool up = q < NQ1;
-      const int kq = up ? (q & 7) : q - NQ1;  // k-step within the current GEMM
-      if (kq == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      const unsigned char* wb = Wt + (q & 1) * D * WROWB;
-      chunk16 wf[4], af[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = w * 64 + i * 16 + (lane & 15);
-        wf[i] = *(const chunk16*)(wb + row * WROWB + wswz(row, lane >> 4) * 16);
-      }
-      const int ca = kq * 4 + (lane >> 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = j * 16 + (lane & 15);
-        af[j] = up ? *(const chunk16*)(P + row * PROWB + pswz(row, ca) * 16)
-                   : *(const chunk16*)(Hh + row * HROWB + hswz(row, ca) * 16);
-      }
-      if (q + NPF < NQ) gload(q + NPF, rb[p]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<bf16>(wf[i], af[j], acc[i][j]);
-      if (q + 1 < NQ) lstore((q + 1) & 1, rb[(p + 1) % NPF]);
-      if (up && kq == 7) {
-        // up-projection N tile done: GELU -> bf16 hidden columns nt*256 + w*64 + i*16 + (lane/16)*4
-        const int nt = q >> 3;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = nt * D + w * 64 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = j * 16 + (lane & 15);
-            const f32x4 a = acc[i][j];
-            const bf16x4 b = {(bf16)gelu_erf(a[0]), (bf16)gelu_erf(a[1]), (bf16)gelu_erf(a[2]), (bf16)gelu_erf(a[3])};
-            *(bf16x4*)(Hh + row * HROWB + hswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = b;
-          }
-        }
-      }
-      if (!up && q == NQ - 1) {
-        // down-projection done: x[m][n .. n+3] += acc  (fp32 residual, in place)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int m = m0 + j * 16 + (lane & 15);
-          if (m >= g.M) continue;
-          float* xr = g.x + xoff(m);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int n = w * 64 + i * 16 + (lane >> 4) * 4;
-            f32x4 v = *(const f32x4*)(xr + n);
-            v += acc[i][j];
-            *(f32x4*)(xr + n) = v;
-          }
-        }
-      }
-      __syncthreads();
+    for (int i = 0; i < NF1; ++i) {
+      const int gg = w * NF1 + i;
+      r[i] = *(const chunk16*)(W1 + ((((int64_t)(gg >> 4) * KS1 + ks) * 16 + (gg & 15)) * 64 + lane) * 8);
     }
+  };
+  chunk16 wb1[NPF1][NF1];
+#pragma unroll
+  for (int p = 0; p < NPF1; ++p) w1load(p, wb1[p]);
+  stamp(1);
+  __syncthreads();  // LN panel complete
+  stamp(2);
+
+  f32x4 acc1[NF1][4];
+#pragma unroll
+  for (int i = 0; i < NF1; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS1; ++ks) {
+    stamp(3 + ks);
+    chunk16 af[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = j * 16 + (lane & 15);
+      af[j] = *(const chunk16*)(P + row * PROWB + xswz(row, ks * 4 + (lane >> 4)) * 16);
+    }
+    chunk16* wf = wb1[ks % NPF1];
+#pragma unroll
+    for (int i = 0; i < NF1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc1[i][j] = mfma_chunk<bf16>(wf[i], af[j], acc1[i][j]);
+    // unconditional refill (the tail reloads the last step): conditional loads make the compiler's
+    // vmcnt bookkeeping drain the whole prefetch
+    w1load(ks + NPF1 < KS1 ? ks + NPF1 : KS1 - 1, wf);
+  }
+
+  stamp(11);
+  // W2 prefetch and the residual rows go out before the GELU epilogue so their latency hides
+  // behind it.  fragment i of wave w = output rows of W2 (w*2+i)*16 .. +15 (one N tile of 256)
+  auto w2load = [&](int ks, chunk16* r) {
+#pragma unroll
+    for (int i = 0; i < NF2; ++i)
+      r[i] = *(const chunk16*)(W2 + ((((int64_t)ks) * 16 + w * NF2 + i) * 64 + lane) * 8);
+  };
+  chunk16 wb2[NPF2][NF2];
+#pragma unroll
+  for (int p = 0; p < NPF2; ++p) w2load(p, wb2[p]);
+  // this lane's 4 rows (j*16 + lane%16) as byte offsets from the panel's first row of x; rows >= M
+  // are out of range for the buffer resource: their residual reads return 0, their stores drop
+  const int64_t xbase = xoff(m0);
+  uint32_t xrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + j * 16 + (lane & 15);
+    xrow[j] = m < g.M ? (uint32_t)((xoff(m) - xbase) * 4) : 0x80000000u;
+  }
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
+  f32x4 res[NF2][4];
+#pragma unroll
+  for (int i = 0; i < NF2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      res[i][j] = __builtin_bit_cast(f32x4, buf_load16(rx, xrow[j] + (uint32_t)(w * 32 + i * 16 + (lane >> 4) * 4) * 4u, 0));
+
+  // GELU -> bf16 hidden image: lane holds hidden columns n .. n+3 of row j*16 + lane%16
+#pragma unroll
+  for (int i = 0; i < NF1; ++i) {
+    const int n = (w * NF1 + i) * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = j * 16 + (lane & 15);
+      const f32x4 a = acc1[i][j];
+      const f32x2 lo = gelu_fast2((f32x2){a[0], a[1]}), hi = gelu_fast2((f32x2){a[2], a[3]});
+      const bf16x4 b = {(bf16)lo[0], (bf16)lo[1], (bf16)hi[0], (bf16)hi[1]};
+      *(bf16x4*)(Hh + row * HROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = b;
+    }
+  }
+  stamp(12);
+  __syncthreads();  // hidden complete
+  stamp(13);
+
+  // ------------------------------------------------------------ FFN-down: 24 k-steps, N 256
+  f32x4 acc2[NF2][4];
+#pragma unroll
+  for (int i = 0; i < NF2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto hread = [&](int ks, chunk16* af) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = j * 16 + (lane & 15);
+      af[j] = *(const chunk16*)(Hh + row * HROWB + xswz(row, ks * 4 + (lane >> 4)) * 16);
+    }
+  };
+  chunk16 ha[2][4];
+  hread(0, ha[0]);
+#pragma unroll
+  for (int ks = 0; ks < KS2; ++ks) {
+    if (ks % 4 == 0) stamp(14 + ks / 4);
+    if (ks + 1 < KS2) hread(ks + 1, ha[(ks + 1) & 1]);  // static condition (loop fully unrolled)
+    chunk16* wf = wb2[ks % NPF2];
+#pragma unroll
+    for (int i = 0; i < NF2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc2[i][j] = mfma_chunk<bf16>(wf[i], ha[ks & 1][j], acc2[i][j]);
+    w2load(ks + NPF2 < KS2 ? ks + NPF2 : KS2 - 1, wf);
+  }
+
+  // x[m][n .. n+3] += acc  (fp32 residual in place; branch-free buffer stores)
+#pragma unroll
+  for (int i = 0; i < NF2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = res[i][j] + acc2[i][j];
+      buf_store16_wt(rx, xrow[j] + (uint32_t)(w * 32 + i * 16 + (lane >> 4) * 4) * 4u, __builtin_bit_cast(u32x4, v));
+    }
+  if constexpr (ST) {
+    stamp(20);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(21);
+    if (samp >= 0) g_ffn_stamps[samp][23] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && blockIdx.x < 1024) g_ffn_wall[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
 }  // namespace
 
 hipError_t launch_ffn(const FfnArgs& g, hipStream_t st) {
-  if (g.M <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ffn_kernel, dim3((g.M + BM - 1) / BM), dim3(256), 0, st, g);
+  if (g.M <= 0 || g.rows_per_seq < 0) return hipErrorInvalidValue;
+  // a panel's rows must lie within the 2 GiB a buffer offset reaches from its first row
+  const int64_t span = g.rows_per_seq ? (BM / g.rows_per_seq + 2) * g.x_seq + (int64_t)BM * D : (int64_t)BM * D;
+  if (span * 4 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+  static const bool stamps = getenv("VAP_FFN_STAMPS") != nullptr;
+  if (stamps)
+    hipLaunchKernelGGL(ffn_kernel<true>, dim3((g.M + BM - 1) / BM), dim3(512), 0, st, g);
+  else
+    hipLaunchKernelGGL(ffn_kernel<false>, dim3((g.M + BM - 1) / BM), dim3(512), 0, st, g);
   return hipGetLastError();
+}
+
+// diagnostics: copy the FFN stamps (8 sampled workgroups x 24) to host memory
+// (8 x 24 sampled phase stamps, then 1024 x 2 per-workgroup wall-clock start / end)
+hipError_t read_ffn_stamps(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ffn_stamps), sizeof(g_ffn_stamps), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(out + 8 * 24, HIP_SYMBOL(g_ffn_wall), sizeof(g_ffn_wall), 0, hipMemcpyDeviceToHost);
 }

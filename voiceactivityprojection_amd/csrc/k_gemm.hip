@@ -238,11 +238,9 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     static const bool v1 = getenv("VAP_GEMM_V1") != nullptr;
     const bool aligned = !(g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 ||
                            (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)));
-    // 256-row tiles when they still fill the chip (~one workgroup per CU) or the K loop is long
-    // enough to amortise the deeper prologue; short-K small-M launches (combinator / heads of a
-    // range) keep 128-row tiles for twice the workgroups
-    const bool big = (int64_t)((M + 255) / 256) * (g.N / BN) >= 200 || g.K >= 512;
-    if (!v1 && aligned && big) return launch_gemm2<TOut>(g, st);
+    // The kernel choice must not depend on M: a clip's outputs are then bit-identical whatever
+    // batch (or shard of a batch) it runs in -- the 128-row kernel accumulates in another order.
+    if (!v1 && aligned) return launch_gemm2<TOut>(g, st);
   }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);

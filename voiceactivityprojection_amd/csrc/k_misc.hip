@@ -379,20 +379,21 @@ hipError_t launch_pack_conv(const float* in, T* out, int N, int C, int KW, hipSt
   hipLaunchKernelGGL((pack_conv_kernel<T>), dim3(256), dim3(256), 0, st, in, out, N, C, KW);
   return hipGetLastError();
 }
-// Row-panel weight layout (k_rowpanel.hip, RowPanelArgs::w_packed): bf16 W [N][256] ->
-// [N/256][8 k-steps][16 row groups][64 lanes][8], lane = (k%32)/8*16 + n%16; one 16-B chunk per thread.
-__global__ void pack_rowpanel_kernel(const chunk16* __restrict__ src, chunk16* __restrict__ dst, int nchunks) {
+// Packed projection-weight layout (k_rowpanel.hip RowPanelArgs::w_packed, k_ffn.hip): bf16 W [N][K]
+// -> [N/256][K/32 k-steps][16 row groups][64 lanes][8], lane = (k%32)/8*16 + n%16: one k-step tile
+// of a 256-row N tile is 16 KiB contiguous and one wave's 16-row MFMA fragment 1 KiB.
+__global__ void pack_rowpanel_kernel(const chunk16* __restrict__ src, chunk16* __restrict__ dst, int nchunks, int ksteps) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= nchunks) return;
-  const int lane = c & 63, grp = (c >> 6) & 15, ks = (c >> 10) & 7, nt = c >> 13;
+  const int lane = c & 63, grp = (c >> 6) & 15, ks = (c >> 10) % ksteps, nt = (c >> 10) / ksteps;
   const int n = nt * 256 + grp * 16 + (lane & 15), kc = ks * 4 + (lane >> 4);
-  dst[c] = src[n * 32 + kc];
+  dst[c] = src[(int64_t)n * ksteps * 4 + kc];
 }
-hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, hipStream_t st) {
-  if (N <= 0 || N % 256) return hipErrorInvalidValue;
-  const int nchunks = N * 32;
+hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, int K, hipStream_t st) {
+  if (N <= 0 || N % 256 || K <= 0 || K % 32) return hipErrorInvalidValue;
+  const int nchunks = N * K / 8;
   hipLaunchKernelGGL(pack_rowpanel_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, st, (const chunk16*)src,
-                     (chunk16*)dst, nchunks);
+                     (chunk16*)dst, nchunks, K / 32);
   return hipGetLastError();
 }
 

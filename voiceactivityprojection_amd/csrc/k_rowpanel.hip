@@ -275,12 +275,12 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
               const uint32_t n = nt * BN + w * 64 + i * 16 + (lane >> 4) * 4;
               f32x4 v = acc[i][j];
               if constexpr (EPI == 1) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+const f32x2 lo = gelu_fast2((f32x2){v[0], v[1]}), hi = gelu_fast2((f32x2){v[2], v[3]});
+                v = f32x4{lo[0], lo[1], hi[0], hi[1]};
               }
               if constexpr (EPI == 2) {
                 v += radd[i][j];
-                buf_store16(rsrc_c, crow[j] + n * 4u, __builtin_bit_cast(u32x4, v));
+                buf_store16_wt(rsrc_c, crow[j] + n * 4u, __builtin_bit_cast(u32x4, v));
               } else {
                 buf_store8(rsrc_c, crow[j] + n * 2u, pack_bf16x4(v[0], v[1], v[2], v[3]));
               }
@@ -295,8 +295,8 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
               const int n = nt * BN + w * 64 + i * 16 + (lane >> 4) * 4;
               f32x4 v = acc[i][j];
               if constexpr (EPI == 1) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+const f32x2 lo = gelu_fast2((f32x2){v[0], v[1]}), hi = gelu_fast2((f32x2){v[2], v[3]});
+                v = f32x4{lo[0], lo[1], hi[0], hi[1]};
               }
               const int64_t co = coff(m) + n;
               if constexpr (EPI == 2) {
@@ -322,7 +322,10 @@ __global__ __launch_bounds__(256, 2) void rowpanel_kernel(RowPanelArgs g) {
 }  // namespace
 
 hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st) {
-  if (g.M <= 0 || g.N % BN != 0 || g.K != KP) return hipErrorInvalidValue;
+  if (g.M <= 0 || g.N % BN != 0 || g.K != KP || g.rows_per_seq < 0) return hipErrorInvalidValue;
+  // the epilogue's buffer offsets reach 2 GiB from a panel's first output row
+  const int64_t span = g.rows_per_seq ? (BM / g.rows_per_seq + 2) * g.c_seq + (int64_t)BM * g.ldc : (int64_t)BM * g.ldc;
+  if (span * (epi == 2 ? 4 : 2) >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
   const dim3 grid((g.M + BM - 1) / BM);
   static const bool v1 = getenv("VAP_RP_V1") != nullptr;
   static const bool stamps = getenv("VAP_RP_STAMPS") != nullptr;

@@ -98,6 +98,12 @@ VAP_DEV void buf_store8(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x2 v) {
 VAP_DEV void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, 0);
 }
+// write-through (sc1) 16-B store: the line leaves the XCD's L2 with the store instead of staying
+// dirty, so the kernel's end-of-launch L2 write-back (~ dirty bytes / 6 TB/s on the next launch's
+// critical path) has nothing to do.  16-B only: narrower sc1 stores are one fabric write each.
+VAP_DEV void buf_store16_wt(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, 16);
+}
 VAP_DEV u32x2 pack_bf16x4(float a, float b, float c, float d) {
   const bf16x4 v = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
   return __builtin_bit_cast(u32x2, v);
@@ -115,4 +121,23 @@ VAP_DEV float gelu_fast(float x) {
   p = fmaf(p, t, 0.254829592f);
   const float h = 0.5f * p * t * __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);  // erfc(z) / 2
   return x * (x >= 0.f ? 1.0f - h : h);
+}
+
+// gelu_fast on two values with packed f32 math (v_pk_mul/v_pk_fma: two lanes' worth per
+// instruction) and the constants folded: z = |x| sqrt(log2e / 2) so that exp(-x^2 / 2) = exp2(-z^2),
+// and GELU = max(x, 0) - |x| erfc(|x| / sqrt2) / 2 = ((x + |x|) - z h) / 2 with the A&S 7.1.26
+// coefficients pre-scaled by 1 / sqrt(log2e / 2) (no sign select, no max).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+VAP_DEV f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 a = __builtin_elementwise_abs(x);
+  const f32x2 z = a * 0.84932180028801907f;
+  const f32x2 d = __builtin_elementwise_fma(z, (f32x2)0.27273748087922250f, (f32x2)1.0f);
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = __builtin_elementwise_fma(t, (f32x2)1.249709390056937f, (f32x2)-1.7109557608284776f);
+  p = __builtin_elementwise_fma(p, t, (f32x2)1.673586784794615f);
+  p = __builtin_elementwise_fma(p, t, (f32x2)-0.334969308339339f);
+  p = __builtin_elementwise_fma(p, t, (f32x2)0.3000389156543292f);
+  const f32x2 e = z * -z;
+  const f32x2 h = p * t * (f32x2){__builtin_amdgcn_exp2f(e[0]), __builtin_amdgcn_exp2f(e[1])};
+  return __builtin_elementwise_fma(-z, h, x + a) * 0.5f;
 }

@@ -52,8 +52,8 @@ struct vap_handle {
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
   bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
-  bool ffn_fused = false;  // VAP_FFN_FUSED=1: bf16 FFN with the hidden in LDS (k_ffn.hip; one workgroup per CU:
-                           // measured 113 us vs 84 us unfused per 32k rows -- kept as an option)
+  bool ffn_fused = true;  // bf16 FFN with the hidden in LDS (k_ffn.hip): 62 us vs 93 us for the unfused
+                          // row-panel up + GEMM down per 32k rows; VAP_FFN_FUSED=0 selects the unfused pair
   hipStream_t side[NSIDE] = {};
   hipEvent_t mb_ev[MAXMB] = {};
   hipEvent_t fork_ev[MAXMB] = {};
@@ -432,11 +432,11 @@ int pack_all(vap_handle* h, hipStream_t st) {
   };
   // bf16: the row-panel projections (K = 256) also get a copy in the packed row-panel layout,
   // "<name>@rp" (one k-step tile 16 KiB contiguous, one wave fragment 1 KiB: k_rowpanel.hip)
-  auto rp_copy = [&](const std::string& name, int N) -> int {
+  auto rp_copy = [&](const std::string& name, int N, int K = D) -> int {
     if constexpr (sizeof(T) == 2) {
-      T* w = alloc(name + "@rp", (int64_t)N * D);
+      T* w = alloc(name + "@rp", (int64_t)N * K);
       if (!w) return fail(VAP_ERR_HIP, "hipMalloc " + name + "@rp");
-      HIPCHK(launch_pack_rowpanel((const bf16*)h->packed.at(name), (bf16*)w, N, st));
+      HIPCHK(launch_pack_rowpanel((const bf16*)h->packed.at(name), (bf16*)w, N, K, st));
     }
     return VAP_OK;
   };
@@ -446,7 +446,9 @@ int pack_all(vap_handle* h, hipStream_t st) {
     if ((rc = cat(p + ".o", {p + ".mha.proj.weight"}))) return rc;
     if ((rc = cat(p + ".w1", {p + ".ffnetwork.0.weight"}))) return rc;
     if ((rc = cat(p + ".w2", {p + ".ffnetwork.3.weight"}))) return rc;
-    if ((rc = rp_copy(p + ".qkv", 3 * D)) || (rc = rp_copy(p + ".o", D)) || (rc = rp_copy(p + ".w1", 3 * D))) return rc;
+    if ((rc = rp_copy(p + ".qkv", 3 * D)) || (rc = rp_copy(p + ".o", D)) || (rc = rp_copy(p + ".w1", 3 * D)) ||
+        (rc = rp_copy(p + ".w2", D, 3 * D)))
+      return rc;
     if (cross) {
       if ((rc = cat(p + ".qc", {p + ".mha_cross.query.weight"}))) return rc;
       if ((rc = cat(p + ".kvc", {p + ".mha_cross.key.weight", p + ".mha_cross.value.weight"}))) return rc;
@@ -535,7 +537,7 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
     if (h->ffn_fused) {
-      FfnArgs f{X, rows, 0, 0, h->W<T>(pre + ".w1"), h->W<T>(pre + ".w2"), h->P(pre + ".ln_ffnetwork.weight"),
+      FfnArgs f{X, rows, 0, 0, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
       HIPCHK(launch_ffn(f, st));
     } else {
@@ -851,7 +853,7 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
     if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
-      FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1"), h->W<T>(pre + ".w2"), h->P(pre + ".ln_ffnetwork.weight"),
+      FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
       HIPCHK(launch_ffn(f, st));
     } else {

@@ -115,6 +115,7 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
                          bf16* out, int64_t out_seq_stride, hipStream_t st, int r0 = 0, int r1 = -1);
 hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CONV01_STAMPS=1)
 hipError_t read_rowpanel_stamps(unsigned long long* out);  // diagnostics (VAP_RP_STAMPS=1)
+hipError_t read_ffn_stamps(unsigned long long* out);  // diagnostics (VAP_FFN_STAMPS=1)
 
 // Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
 // amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).
@@ -140,10 +141,11 @@ struct RowPanelArgs {
   int w_packed = 0;
 };
 hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st);
-hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, hipStream_t st);  // K = 256 (k_misc.hip)
+hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, int K, hipStream_t st);  // (k_misc.hip)
 
 // Fused FFN block (k_ffn.hip, bf16): x += W2 . GELU(W1 . LayerNorm(x)), x fp32 [rows][256] in place,
-// W1 [768][256], W2 [256][768] bf16.  Row addressing as RowPanelArgs (rows_per_seq / x_seq).
+// W1 [768][256] and W2 [256][768] bf16 in the PACKED projection layout (launch_pack_rowpanel with
+// K = 256 / 768).  Row addressing as RowPanelArgs (rows_per_seq / x_seq).
 struct FfnArgs {
   float* x;
   int M;

@@ -119,12 +119,35 @@ int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, i
   return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
 }
 
-int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream) {
-  FfnArgs g{x, M, 0, 0, W1, W2, gamma, beta, 1e-5f};
+int vap_test_pack_weight(const void* W, void* out, int N, int K, void* stream) {
+  return rc_of(launch_pack_rowpanel((const bf16*)W, (bf16*)out, N, K, (hipStream_t)stream));
+}
+int vap_test_ffn_packed(float* x, int M, const void* W1p, const void* W2p, const float* gamma, const float* beta,
+                        void* stream) {
+  FfnArgs g{x, M, 0, 0, W1p, W2p, gamma, beta, 1e-5f};
   return rc_of(launch_ffn(g, (hipStream_t)stream));
+}
+int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream) {
+  // W1 / W2 arrive in the plain [N][K] layout: pack them as the engine does at weight load
+  hipStream_t st = (hipStream_t)stream;
+  void *p1 = nullptr, *p2 = nullptr;
+  const size_t n = 768 * 256 * sizeof(bf16);
+  if (hipMalloc(&p1, n) != hipSuccess || hipMalloc(&p2, n) != hipSuccess) {
+    (void)hipFree(p1);
+    return VAP_ERR_HIP;
+  }
+  hipError_t e = launch_pack_rowpanel((const bf16*)W1, (bf16*)p1, 768, 256, st);
+  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)W2, (bf16*)p2, 256, 768, st);
+  FfnArgs g{x, M, 0, 0, p1, p2, gamma, beta, 1e-5f};
+  if (e == hipSuccess) e = launch_ffn(g, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(p1);
+  (void)hipFree(p2);
+  return rc_of(e);
 }
 
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
+int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
 
 }  // extern "C"
