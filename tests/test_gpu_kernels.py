@@ -36,8 +36,12 @@ def _p(t):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("case", ["plain", "conv_cn_relu", "resid", "ln_gelu", "gelu"])
+@pytest.mark.parametrize("case", ["plain", "conv_cn_relu", "resid", "ln_gelu", "gelu", "comb", "many_tiles",
+                                  "many_tiles_n1024"])
 def test_gemm(prec, case):
+    """Implicit-conv GEMM with every epilogue form.  comb = act(LN(A W)) + residual (the combinator's
+    second half); many_tiles* = more 256-row tiles than CUs, so persistent workgroups walk several
+    tiles with the DMA stream running across the tile seams (N 256 and N 1024)."""
     N = lib()
     code, dt = PREC[prec]
     g = torch.Generator().manual_seed(1)
@@ -47,6 +51,12 @@ def test_gemm(prec, case):
         S, Mps, K, Nn, lda = 3, 77, 1024, 256, 512
     elif case in ("resid", "gelu"):
         S, Mps, K, Nn, lda = 2, 130, 768, 256, 768
+    elif case == "comb":
+        S, Mps, K, Nn, lda = 2, 300, 256, 256, 256
+    elif case == "many_tiles":
+        S, Mps, K, Nn, lda = 2, 40000, 256, 256, 256
+    elif case == "many_tiles_n1024":
+        S, Mps, K, Nn, lda = 1, 20000, 256, 1024, 256
     else:
         S, Mps, K, Nn, lda = 2, 201, 1280, 256, 512
     L = (Mps - 1) * lda + K
@@ -64,8 +74,8 @@ def test_gemm(prec, case):
     X = Ar[:, idx]  # (S, Mps, K) overlapping rows
     ref = X @ Wr.T
     norm = act = 0
-    use_bias = case != "plain"
-    use_add = case == "resid"
+    use_bias = case not in ("plain", "comb", "many_tiles")
+    use_add = case in ("resid", "comb")
     if use_bias:
         ref = ref + bias
     if case == "conv_cn_relu":
@@ -73,7 +83,7 @@ def test_gemm(prec, case):
         mu = ref.mean(-1, keepdim=True)
         var = ref.var(-1, keepdim=True)
         ref = torch.relu((ref - mu) * torch.rsqrt(var + 1e-5) * gamma + beta)
-    elif case == "ln_gelu":
+    elif case in ("ln_gelu", "comb"):
         norm, act = 2, 2
         ref = F.gelu(F.layer_norm(ref, (Nn,), gamma, beta))
     elif case == "gelu":
@@ -81,7 +91,7 @@ def test_gemm(prec, case):
         ref = F.gelu(ref)
     if use_add:
         ref = ref + add
-    out_f32 = 1 if (prec == "fp32" or case in ("resid", "ln_gelu")) else 0
+    out_f32 = 1 if (prec == "fp32" or case in ("resid", "ln_gelu", "comb")) else 0
     C = torch.zeros(S, Mps, Nn, device="cuda", dtype=torch.float32 if out_f32 else dt)
     Ad, Wd = Aq.cuda(), Wq.cuda()
     bd, gd, bed, addd = bias.cuda(), gamma.cuda(), beta.cuda(), add.cuda()

@@ -56,9 +56,19 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   }
   const unsigned char* Ab = (const unsigned char*)A;
   const unsigned char* Wb = (const unsigned char*)W;
+  // k-step order: with overlapping implicit-conv rows (lda < K, K = taps x 256), tap-inner order
+  // (256-channel block outer) makes row t's tap j+2 -- the same input row as row t+1's tap j -- be
+  // read two k-steps later instead of 16, while it is still in L2 (sequential order fetched the
+  // input twice from HBM).  Only the summation order changes.
+  const int taps = g.lda < g.K && g.K % 256 == 0 ? g.K / 256 : 1;
+  auto koff = [&](int kt) -> uint32_t {  // byte offset of k-step kt within a row
+    if (taps == 1) return (uint32_t)kt * ROWB;
+    const int cb = kt / taps, tap = kt - cb * taps;
+    return (uint32_t)(tap * 256 + cb * BK) * 2;
+  };
   auto dma = [&](int kt) {
     unsigned char* base = smem + (kt % NST) * STAGE;
-    const uint32_t kb = (uint32_t)kt * ROWB;
+    const uint32_t kb = koff(kt);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(Ab + (aoff[i] + kb)), (lds_void*)(base + (wave * 2 + i) * 1024), 16, 0, 0);
@@ -203,9 +213,11 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[j][i][r] = gelu_erf(acc[j][i][r]);
+      for (int i = 0; i < 8; ++i) {
+        const f32x2 lo = gelu_fast2((f32x2){acc[j][i][0], acc[j][i][1]});
+        const f32x2 hi = gelu_fast2((f32x2){acc[j][i][2], acc[j][i][3]});
+        acc[j][i] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
   }
   TOut* __restrict__ C = (TOut*)g.C;
 #pragma unroll
