@@ -80,6 +80,25 @@ int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t
 int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
                 float* vad_logits, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Rolling-window stream (SURVEY config C5; replaces the reference's per-hop model.probs(x) on a
+ * rolled window, sds/run_sds.py:206-241 TurnTakingSDS.add_audio_bytes_to_tensor / run, and the
+ * fold loop of run.py:23-131 step_extraction).  The stream owns its window [B][2][window] (zeros
+ * at creation) and workspace.  A push rolls `hop` new samples per channel into the window (hop
+ * audio [B][2][hop], device) and writes logits [B][T][256] / vad_logits [B][T][2] of the WHOLE
+ * window, equal to vap_forward on that window.  In bf16 mode with hop % 160 == 0, the CPC conv rows
+ * whose receptive field stays inside the window are carried over from the previous push instead of
+ * recomputed (the conv stack is shift-equivariant with stride 160). */
+typedef struct vap_stream vap_stream;
+int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t hop_samples, void* stream,
+                      vap_stream** out);
+int vap_stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad_logits, void* stream);
+/* frames T of a window, window / hop samples, conv4 rows carried over per push, current window (device). */
+int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, int64_t* hop_samples,
+                    int64_t* reused_rows, const float** window);
+/* Window back to zeros; the next push recomputes every row. */
+int vap_stream_reset(vap_stream* s, void* stream);
+void vap_stream_destroy(vap_stream* s);
+
 /* EncoderCPC.encode_audio (vap/model.py:169-175): out [2][B][T][256] = (x1, x2). */
 int vap_encode(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* out, void* workspace,
                size_t workspace_bytes, void* stream);
@@ -150,6 +169,8 @@ int vap_test_read_rp_stamps(unsigned long long* out);
 /* timing diagnostics (VAP_FFN_STAMPS=1): 8 x 24 s_memtime stamps of sampled fused-FFN workgroups, then
  * 1024 x 2 s_memrealtime start / end of every workgroup (out holds 2240 values) */
 int vap_test_read_ffn_stamps(unsigned long long* out);
+/* timing diagnostics: 8 x 2 x 4 x 6 s_memtime stamps of sampled bf16 GEMM k-steps (VAP_GEMM2_STAMPS=1) */
+int vap_test_read_gemm_stamps(unsigned long long* out);
 
 #ifdef __cplusplus
 }

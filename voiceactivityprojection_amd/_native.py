@@ -44,6 +44,11 @@ _SIGS = {
     "vap_workspace_size": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.POINTER(ctypes.c_size_t)]),
     "vap_forward": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, _P, ctypes.c_size_t, _P]),
     "vap_encode": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, ctypes.c_size_t, _P]),
+    "vap_stream_create": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P]),
+    "vap_stream_push": (ctypes.c_int, [_P, _P, _P, _P, _P]),
+    "vap_stream_info": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "vap_stream_reset": (ctypes.c_int, [_P, _P]),
+    "vap_stream_destroy": (None, [_P]),
     "vap_probs": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "vap_aggregate": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]),
@@ -65,6 +70,7 @@ _SIGS = {
     "vap_test_read_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_rp_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_ffn_stamps": (ctypes.c_int, [_P]),
+    "vap_test_read_gemm_stamps": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_ffn_packed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),

@@ -17,6 +17,8 @@
 //     that share each SIMD (one reads fragments while the other runs its MFMAs);
 //   * operands swapped (C^T = W A^T) so a lane owns 4 consecutive columns of one row: 8-byte bf16 /
 //     16-byte fp32 stores and residual loads, row statistics by a 16-lane-stride shuffle + LDS.
+#include <cstdlib>
+
 #include "vap_common.h"
 #include "vap_kernels.h"
 
@@ -30,7 +32,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 // 64-byte rows, 4 chunks: conflict-free ds_read_b128 for 16 consecutive rows x 4 chunks
 VAP_DEV int swz(int row, int c) { return c ^ ((row >> 2) & 2); }
 
-template <typename TOut>
+// diagnostics (VAP_GEMM2_STAMPS=1): waves 0 and 4 of workgroups 0, 64, .., 448 record s_memtime at
+// k-steps 8..11: [LOAD start, fragments in, after LOAD barrier, MFMAs done, DMA wait done, after
+// COMPUTE barrier] -> g_g2_stamps[wg][wave 0/4][4 k-steps][6]
+__device__ unsigned long long g_g2_stamps[8][2][4][6];
+
+template <typename TOut, bool ST = false>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -39,6 +46,16 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const bf16* __restrict__ A = (const bf16*)g.A;
   const bf16* __restrict__ W = (const bf16*)g.W;
+  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && blockIdx.y == 0 && (lane == 0) &&
+                    (wave == 0 || wave == 4))
+                       ? (int)(blockIdx.x >> 6)
+                       : -1;
+  auto stamp = [&](int kt, int k) {
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (samp >= 0 && kt >= 8 && kt < 12) g_g2_stamps[samp][wave >> 2][kt - 8][k] = t;
+    }
+  };
 
   // DMA sources: a piece (one wave instruction, 1 KiB) = 16 rows x 64 B; wave w fills pieces 2w and
   // 2w+1 of each operand image; lane -> (row 16p + lane/4, physical chunk lane%4) holding logical
@@ -107,6 +124,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     // ---- LOAD
     __builtin_amdgcn_sched_barrier(0);
+    stamp(kt, 0);
     if (kt + NST - 1 < nk) dma(kt + NST - 1);
     const unsigned char* abase = smem + (kt % NST) * STAGE;
     const unsigned char* bbase = abase + BM * ROWB;
@@ -123,7 +141,9 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    stamp(kt, 1);
     __builtin_amdgcn_s_barrier();
+    stamp(kt, 2);
     // ---- COMPUTE
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -133,11 +153,14 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
       for (int i = 0; i < 8; ++i) acc[j][i] = mfma_chunk<bf16>(wf[j], af[i], acc[j][i]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    stamp(kt, 3);
     // own DMA of stage kt+1 landed: newer DMAs are those of stages kt+2 and kt+3 (4 each, if issued)
     if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(kt, 4);
     __builtin_amdgcn_s_barrier();
+    stamp(kt, 5);
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -247,8 +270,17 @@ hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
   if (g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 || (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)))
     return hipErrorInvalidValue;
   dim3 grid((M + BM - 1) / BM, g.N / BN);
-  hipLaunchKernelGGL((gemm2_kernel<TOut>), grid, dim3(512), 0, st, g);
+  static const bool stamps = getenv("VAP_GEMM2_STAMPS") != nullptr;
+  if (stamps)
+    hipLaunchKernelGGL((gemm2_kernel<TOut, true>), grid, dim3(512), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<TOut, false>), grid, dim3(512), 0, st, g);
   return hipGetLastError();
+}
+
+// diagnostics: copy the gemm2 k-step stamps (8 x 2 x 4 x 6) to host memory
+hipError_t read_gemm2_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_g2_stamps), sizeof(g_g2_stamps), 0, hipMemcpyDeviceToHost);
 }
 
 template hipError_t launch_gemm2<bf16>(const GemmArgs&, hipStream_t);

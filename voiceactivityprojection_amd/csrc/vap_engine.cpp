@@ -876,92 +876,66 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
 // chunk c (downsample, every transformer layer on the chunk's frames -- causal, so only earlier
 // keys are needed) waits for done[c].  The serial LSTM thus overlaps the whole front end and the
 // earlier chunks' back ends, for all clips at once.
-int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, float* logits, float* vadl,
-                   unsigned char* ws, hipStream_t st) {
-  using T = bf16;
-  const int S = p.S, T_ = p.T;
-  const int64_t* L = p.L;
-  const std::string g = "encoder.encoder.gEncoder";
-  int nch = std::min(h->time_chunks, vap_handle::MAXMB);
-  nch = std::max(1, std::min(nch, T_ / 32));  // chunks of at least 32 frames
-  // frame chunks [fb[c], fb[c+1]) and LSTM step chunk ends
-  int fb[vap_handle::MAXMB + 1];
-  for (int c = 0; c <= nch; ++c) fb[c] = (int)((int64_t)T_ * c / nch);
-  LstmSync sy{};
+// Time-chunk schedule of a plan: frame chunks [fb[c], fb[c+1]) and the LSTM step at which each ends.
+struct TcSched {
+  int nch = 1;
+  int fb[vap_handle::MAXMB + 1]{};
+  int seq_end[vap_handle::MAXMB]{};
+};
+TcSched tc_schedule(const vap_handle* h, const Plan& p) {
+  TcSched t;
+  const int T_ = p.T;
+  t.nch = std::min(h->time_chunks, vap_handle::MAXMB);
+  t.nch = std::max(1, std::min(t.nch, T_ / 32));  // chunks of at least 32 frames
+  for (int c = 0; c <= t.nch; ++c) t.fb[c] = (int)((int64_t)T_ * c / t.nch);
+  for (int c = 0; c < t.nch; ++c)
+    t.seq_end[c] = c + 1 == t.nch ? (int)p.L[4] : std::min((int)p.L[4], 2 * t.fb[c + 1]);
+  return t;
+}
+
+// The recurrence of the time-chunked forward: ONE persistent launch on a side stream covers every
+// sequence, waiting at each chunk boundary for ready[c] and publishing done[c].
+int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* GX, unsigned char* ws, LstmSync& sy,
+                   hipStream_t st) {
+  sy = LstmSync{};
   sy.ready = h->sync_mem;
   sy.done = h->sync_mem + vap_handle::MAXMB;
   sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
   sy.epoch = ++h->epoch;
-  sy.nr = nch;
+  sy.nr = t.nch;
   sy.time_mode = 1;
-  for (int c = 0; c < nch; ++c) sy.seq_end[c] = c + 1 == nch ? (int)L[4] : std::min((int)L[4], 2 * fb[c + 1]);
-  const int nwg = (S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
-  for (int c = 0; c < nch; ++c) h->done_expect[c] += nwg;
-
-  // the recurrence: one launch, every sequence, gated by the ready flags
+  for (int c = 0; c < t.nch; ++c) sy.seq_end[c] = t.seq_end[c];
+  const int nwg = (p.S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
+  for (int c = 0; c < t.nch; ++c) h->done_expect[c] += nwg;
   hipStream_t side = h->side[0];
   hipEvent_t fork = h->next_fork_event();
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
-  T* GX = (T*)(ws + p.GX);
-  {
-    Timed tm(h, VAP_K_LSTM_REC, side);
-    HIPCHK(launch_lstm_resident(GX, S, (int)L[4], h->W<T>("whh_l0"), (T*)(ws + p.H0) + 4 * D, p.sh, side, &sy));
-  }
+  Timed tm(h, VAP_K_LSTM_REC, side);
+  HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy));
+  return VAP_OK;
+}
 
-  // ---- front end, chunk by chunk
-  T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
-  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
-  int64_t done_rows[4] = {0, 0, 0, 0};
-  for (int c = 0; c < nch; ++c) {
-    int64_t e[4];
-    e[3] = sy.seq_end[c];
-    for (int i = 2; i >= 0; --i) e[i] = c + 1 == nch ? L[i + 1] : std::min(L[i + 1], 2 * e[i + 1] + 1);
-    if (e[0] > done_rows[0]) {
-      Timed tm(h, VAP_K_CONV1, st);
-      HIPCHK(launch_conv01(wav, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"), h->fpacked.at("conv0_stat"),
-                           h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), h->P(g + ".conv1.bias"),
-                           h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"), (bf16*)(Xs[0] + D), p.s1, st,
-                           (int)done_rows[0], (int)e[0]));
-    }
-    for (int i = 1; i < 4; ++i) {  // conv2..4: implicit GEMMs on the new rows (encoder_components.py:100-103)
-      const int64_t a = done_rows[i], b = e[i];
-      if (b <= a) continue;
-      const std::string cs = std::to_string(i + 1);
-      Timed tm(h, VAP_K_CONV234, st);
-      GemmArgs ga = gargs(Xs[i - 1] + a * 2 * D, 2 * D, ss[i - 1], h->W<T>("conv" + cs), 4 * D, D,
-                          h->P(g + ".conv" + cs + ".bias"), (int)(b - a), S, Xs[i] + D + a * D, D, ss[i]);
-      ga.norm = 1;
-      ga.act = 1;
-      ga.gamma = h->P(g + ".batchNorm" + cs + ".weight");
-      ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
-      HIPCHK(gemm<T>(ga, st, false));
-    }
-    {  // LSTM gate projection of the new steps
-      const int64_t a = done_rows[3], b = e[3];
-      Timed tm(h, VAP_K_LSTM_PROJ, st);
-      HIPCHK(gemm<T>(gargs(Xs[3] + D + a * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)(b - a),
-                           S, GX + a * 4 * D, 4 * D, L[4] * 4 * D), st, false));
-    }
-    for (int i = 0; i < 4; ++i) done_rows[i] = e[i];
-    HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
-  }
-
-  // ---- back end, chunk by chunk: on its own stream (bst) so that chunk c's transformer overlaps
-  // the front ends of the later chunks (the kernels of either side leave CUs / pipes idle in their
-  // prologues, epilogues and phase barriers); the LSTM hand-off orders them
+// Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
+// every transformer layer on the chunk's frames; then heads over all clips and the join.
+int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& sy, unsigned char* ws, float* logits,
+                float* vadl, hipStream_t st) {
+  using T = bf16;
+  const int S = p.S, T_ = p.T;
   const int64_t t1 = (int64_t)T_ * D;
   T* Hf = (T*)(ws + p.H0);
   float* X = (float*)(ws + p.X);
+  // with tc_streams >= 2 the back end runs on its own stream so chunk c's transformer may overlap the
+  // later chunks' front ends; the LSTM hand-off orders them
   hipStream_t bst = h->tc_streams >= 2 ? h->side[1] : st;
   if (bst != st) {
-    hipEvent_t fk = h->next_fork_event();  // the back-end stream starts after this call's set-up
+    hipEvent_t fk = h->next_fork_event();
     HIPCHK(hipEventRecord(fk, st));
     HIPCHK(hipStreamWaitEvent(bst, fk, 0));
   }
   int rc;
-  for (int c = 0; c < nch; ++c) {
-    const int f0 = fb[c], f1 = fb[c + 1];
+  for (int c = 0; c < t.nch; ++c) {
+    const int f0 = t.fb[c], f1 = t.fb[c + 1];
     HIPCHK(hipStreamWaitValue32(bst, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
     {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
       Timed tm(h, VAP_K_DOWNSAMPLE, bst);
@@ -980,13 +954,80 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
       if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst))) return rc;
   }
   if ((rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst))) return rc;
-  HIPCHK(hipEventRecord(h->mb_ev[0], side));  // join: the LSTM launch has fully retired
+  HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
   if (bst != st) {
     HIPCHK(hipEventRecord(h->mb_ev[1], bst));
     HIPCHK(hipStreamWaitEvent(st, h->mb_ev[1], 0));
   }
   return VAP_OK;
+}
+
+// bf16 CPC rows of conv4 range [a4, b4) of every sequence, with the conv1..conv3 rows they need
+// (k4 s2 p1 layers: rows [a, b) need input rows [2a-1, 2b+1) clipped to the layer; conv1 rows come
+// from the fused conv0->conv1 kernel straight from the waveform), then their LSTM gate projections.
+int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigned char* ws, bf16* GX, int64_t a4,
+              int64_t b4, hipStream_t st) {
+  using T = bf16;
+  const int S = p.S;
+  const int64_t* L = p.L;
+  const std::string g = "encoder.encoder.gEncoder";
+  T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
+  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
+  int64_t a[4], b[4];
+  a[3] = a4;
+  b[3] = b4;
+  for (int i = 2; i >= 0; --i) {
+    a[i] = std::max<int64_t>(0, 2 * a[i + 1] - 1);
+    b[i] = std::min(L[i + 1], 2 * b[i + 1] + 1);
+  }
+  {
+    Timed tm(h, VAP_K_CONV1, st);
+    HIPCHK(launch_conv01(wav, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"), h->fpacked.at("conv0_stat"),
+                         h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), h->P(g + ".conv1.bias"),
+                         h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"), (bf16*)(Xs[0] + D), p.s1, st,
+                         (int)a[0], (int)b[0]));
+  }
+  for (int i = 1; i < 4; ++i) {  // conv2..4 (encoder_components.py:100-103)
+    const std::string cs = std::to_string(i + 1);
+    Timed tm(h, VAP_K_CONV234, st);
+    GemmArgs ga = gargs(Xs[i - 1] + a[i] * 2 * D, 2 * D, ss[i - 1], h->W<T>("conv" + cs), 4 * D, D,
+                        h->P(g + ".conv" + cs + ".bias"), (int)(b[i] - a[i]), S, Xs[i] + D + a[i] * D, D, ss[i]);
+    ga.norm = 1;
+    ga.act = 1;
+    ga.gamma = h->P(g + ".batchNorm" + cs + ".weight");
+    ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
+    HIPCHK(gemm<T>(ga, st, false));
+  }
+  Timed tm(h, VAP_K_LSTM_PROJ, st);
+  HIPCHK(gemm<T>(gargs(Xs[3] + D + a4 * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)(b4 - a4),
+                       S, GX + a4 * 4 * D, 4 * D, L[4] * 4 * D), st, false));
+  return VAP_OK;
+}
+
+// VapGPT.forward pipelined ALONG TIME (bf16, 1-layer LSTM).  The frames are cut into `nch` chunks;
+// on the caller's stream the front end of chunk c computes only the conv / gate-projection rows
+// that chunk needs (receptive fields: conv4 rows [., e) need conv3 rows < 2e+1, and so on down to
+// conv1), then publishes ready[c]; one persistent LSTM launch on a side stream runs every
+// sequence's recurrence, waiting at each chunk boundary and publishing done[c]; the back end of
+// chunk c (downsample, every transformer layer on the chunk's frames -- causal, so only earlier
+// keys are needed) waits for done[c].  The serial LSTM thus overlaps the whole front end and the
+// earlier chunks' back ends, for all clips at once.
+int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, float* logits, float* vadl,
+                   unsigned char* ws, hipStream_t st) {
+  using T = bf16;
+  const TcSched t = tc_schedule(h, p);
+  T* GX = (T*)(ws + p.GX);
+  LstmSync sy;
+  int rc;
+  if ((rc = tc_launch_lstm(h, p, t, GX, ws, sy, st))) return rc;
+  int64_t done_rows = 0;
+  for (int c = 0; c < t.nch; ++c) {  // front end, chunk by chunk
+    if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st))) return rc;
+    done_rows = t.seq_end[c];
+    HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
+  }
+  return tc_back_end(h, p, t, sy, ws, logits, vadl, st);
 }
 
 // VapGPT.forward (model.py:249-268).  Micro-batch pipeline: the batch is split into up to
@@ -1096,7 +1137,114 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   return VAP_OK;
 }
 
+
+// ------------------------------------------------------------------------ streaming (C5)
+// Conv4 row r of a window of n samples is CLEAN when no layer of its receptive field reaches a
+// padding row or sample: k4 s2 p1 rows [lo, hi) need input rows [2lo-1, 2hi+1), conv1 (k8 s4 p2)
+// [4lo-2, 4hi+2), conv0 (k10 s5 p3) samples [5lo-3, 5hi+2).  A clean row depends only on the samples
+// under it, so after a hop of h = 160 k samples new row r equals old row r + k whenever both are
+// clean (the conv stack is shift-equivariant with stride 160).
+bool conv4_row_clean(const int64_t* L, int64_t n, int64_t r) {
+  int64_t lo = r, hi = r + 1;
+  for (int lvl = 3; lvl >= 1; --lvl) {  // conv4 -> conv3 -> conv2 -> conv1 input rows
+    lo = 2 * lo - 1;
+    hi = 2 * hi + 1;
+    if (lo < 0 || hi > L[lvl]) return false;
+  }
+  lo = 4 * lo - 2;  // conv1 -> conv0 rows
+  hi = 4 * hi + 2;
+  if (lo < 0 || hi > L[0]) return false;
+  lo = 5 * lo - 3;  // conv0 -> samples
+  hi = 5 * hi + 2;
+  return lo >= 0 && hi <= n;
+}
+
 }  // namespace
+
+// Rolling-window stream (sds/run_sds.py:206-241 TurnTakingSDS.run: x.roll(-hop) + new samples at
+// the end, model.probs(x) on the whole window; SURVEY config C5).  The window starts as zeros.  A
+// push shifts the window by one hop; in bf16 mode the LSTM gate projections of the conv4 rows
+// whose receptive field stays clean are carried over (shifted by hop/160 rows) and only the rows
+// at the window edges -- the new audio plus the zero-padded first row -- run through the CPC conv
+// stack.  The recurrence (zero state at the window start) and the transformer are recomputed, as
+// in the reference, so the outputs equal a full forward of the window.
+struct vap_stream {
+  vap_handle* h = nullptr;
+  int B = 0;
+  int64_t W = 0, hop = 0;
+  int hop_rows = 0;
+  Plan p;
+  unsigned char* ws = nullptr;
+  float* win[2] = {};
+  bf16* gx[2] = {};
+  int cur = 0;
+  int64_t pushes = 0;
+  int64_t keep0 = 0, keep1 = 0;  // conv4 rows [keep0, keep1) carried over from the previous window
+  bool reuse = false;
+  ~vap_stream() {
+    (void)hipFree(ws);
+    for (int i = 0; i < 2; ++i) {
+      (void)hipFree(win[i]);
+      (void)hipFree(gx[i]);
+    }
+  }
+};
+
+namespace {
+
+int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vadl, hipStream_t st) {
+  vap_handle* h = s->h;
+  const Plan& p = s->p;
+  const int S = p.S;
+  const int nxt = 1 - s->cur;
+  const int64_t W = s->W, hop = s->hop, L4 = p.L[4];
+  // roll: window[:, :W-hop] = old window[:, hop:], window[:, W-hop:] = the new samples
+  HIPCHK(hipMemcpy2DAsync(s->win[nxt], W * sizeof(float), s->win[s->cur] + hop, W * sizeof(float),
+                          (W - hop) * sizeof(float), S, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpy2DAsync(s->win[nxt] + (W - hop), W * sizeof(float), hop_audio, hop * sizeof(float),
+                          hop * sizeof(float), S, hipMemcpyDeviceToDevice, st));
+  const float* wav = s->win[nxt];
+  int rc;
+  if (!s->reuse) {  // fp32 parity mode / no time-chunked path: full forward of the window
+    rc = h->dims.precision == VAP_PRECISION_BF16 ? run_forward<bf16>(h, wav, s->B, W, logits, vadl, s->ws, st)
+                                                 : run_forward<float>(h, wav, s->B, W, logits, vadl, s->ws, st);
+    if (rc) return rc;
+    s->cur = nxt;
+    ++s->pushes;
+    return VAP_OK;
+  }
+  bf16* GX = s->gx[nxt];
+  const TcSched t = tc_schedule(h, p);
+  LstmSync sy;
+  if ((rc = tc_launch_lstm(h, p, t, GX, s->ws, sy, st))) return rc;
+  if (s->pushes > 0 && s->keep1 > s->keep0) {
+    // carried-over gate projections: new row r = old row r + hop_rows
+    const size_t row = 4 * D * sizeof(bf16);
+    HIPCHK(hipMemcpy2DAsync(GX + s->keep0 * 4 * D, L4 * row, s->gx[s->cur] + (s->keep0 + s->hop_rows) * 4 * D, L4 * row,
+                            (s->keep1 - s->keep0) * row, S, hipMemcpyDeviceToDevice, st));
+    if (s->keep0 > 0 && (rc = conv_rows(h, p, wav, W, s->ws, GX, 0, s->keep0, st))) return rc;
+    if ((rc = conv_rows(h, p, wav, W, s->ws, GX, s->keep1, L4, st))) return rc;
+  } else if ((rc = conv_rows(h, p, wav, W, s->ws, GX, 0, L4, st))) {
+    return rc;
+  }
+  for (int c = 0; c < t.nch; ++c) HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
+  if ((rc = tc_back_end(h, p, t, sy, s->ws, logits, vadl, st))) return rc;
+  s->cur = nxt;
+  ++s->pushes;
+  return VAP_OK;
+}
+
+int stream_zero(vap_stream* s, hipStream_t st) {
+  const Plan& p = s->p;
+  const int S = p.S;
+  for (int i = 0; i < 2; ++i) HIPCHK(hipMemsetAsync(s->win[i], 0, (size_t)S * s->W * sizeof(float), st));
+  s->cur = 0;
+  s->pushes = 0;
+  return VAP_OK;
+}
+
+}  // namespace
+
 
 // ============================================================================== C ABI
 extern "C" {
@@ -1215,6 +1363,85 @@ int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_sampl
              : run_forward<float>(h, waveform, batch, n_samples, logits, vad_logits, (unsigned char*)workspace,
                                   (hipStream_t)stream);
 }
+
+int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t hop_samples, void* stream,
+                      vap_stream** out) {
+  if (!h || !out) return fail(VAP_ERR_INVALID, "null argument");
+  if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
+  if (batch <= 0 || window_samples <= 0 || hop_samples <= 0 || hop_samples > window_samples)
+    return fail(VAP_ERR_INVALID, "bad batch / window / hop");
+  int64_t L[6];
+  frame_lengths(window_samples, L);
+  if (L[5] <= 0) return fail(VAP_ERR_INVALID, "window too short for one frame");
+  hipStream_t st = (hipStream_t)stream;
+  auto* s = new vap_stream;
+  s->h = h;
+  s->B = batch;
+  s->W = window_samples;
+  s->hop = hop_samples;
+  s->p = plan_for(h, batch, window_samples);
+  const Plan& p = s->p;
+  const int S = p.S;
+  auto bail = [&](const char* what) {
+    delete s;
+    return fail(VAP_ERR_HIP, std::string("vap_stream_create: ") + what);
+  };
+  if (hipMalloc(&s->ws, p.total) != hipSuccess) return bail("workspace");
+  for (int i = 0; i < 2; ++i)
+    if (hipMalloc(&s->win[i], (size_t)S * window_samples * sizeof(float)) != hipSuccess) return bail("window");
+  // carry-over is exact only for hops of whole conv4 rows (160 samples) on the time-chunked bf16 path
+  const bool bf = h->dims.precision == VAP_PRECISION_BF16;
+  if (bf && h->use_time_chunks() && h->ensure_streams()) return bail("streams");  // sets wait_value
+  s->reuse = bf && h->use_time_chunks() && h->wait_value && hop_samples % 160 == 0;
+  if (const char* e = getenv("VAP_STREAM_REUSE")) s->reuse = s->reuse && atoi(e) != 0;  // A/B: 0 = recompute
+  if (s->reuse) {
+    for (int i = 0; i < 2; ++i)
+      if (hipMalloc(&s->gx[i], (size_t)S * L[4] * 4 * D * sizeof(bf16)) != hipSuccess) return bail("gate buffers");
+    s->hop_rows = (int)(hop_samples / 160);
+    int64_t c0 = 0;
+    while (c0 < L[4] && !conv4_row_clean(L, window_samples, c0)) ++c0;
+    int64_t c1 = c0;
+    while (c1 < L[4] && conv4_row_clean(L, window_samples, c1)) ++c1;
+    s->keep0 = c0;
+    s->keep1 = std::max(c0, c1 - s->hop_rows);  // new row r and old row r + hop_rows both clean
+    // the persistent workspace's conv / LSTM pad rows are zero once and never written
+    bf16* Xs[4] = {(bf16*)(s->ws + p.X1), (bf16*)(s->ws + p.X2), (bf16*)(s->ws + p.X3), (bf16*)(s->ws + p.X4)};
+    const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
+    for (int i = 0; i < 4; ++i) {
+      if (launch_zero_rows<bf16>(Xs[i], S, ss[i], 1, st) != hipSuccess ||
+          launch_zero_rows<bf16>(Xs[i] + (L[i + 1] + 1) * D, S, ss[i], 1, st) != hipSuccess)
+        return bail("zero rows");
+    }
+    if (launch_zero_rows<bf16>((bf16*)(s->ws + p.H0), S, p.sh, 4, st) != hipSuccess) return bail("zero rows");
+  }
+  if (stream_zero(s, st)) return bail("zero window");
+  if (hipStreamSynchronize(st) != hipSuccess) return bail("sync");
+  *out = s;
+  return VAP_OK;
+}
+
+int vap_stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad_logits, void* stream) {
+  if (!s || !hop_audio || !logits || !vad_logits) return fail(VAP_ERR_INVALID, "null argument");
+  return stream_push(s, hop_audio, logits, vad_logits, (hipStream_t)stream);
+}
+
+int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, int64_t* hop_samples,
+                    int64_t* reused_rows, const float** window) {
+  if (!s) return fail(VAP_ERR_INVALID, "null stream");
+  if (frames) *frames = s->p.T;
+  if (window_samples) *window_samples = s->W;
+  if (hop_samples) *hop_samples = s->hop;
+  if (reused_rows) *reused_rows = s->reuse ? s->keep1 - s->keep0 : 0;
+  if (window) *window = s->win[s->cur];
+  return VAP_OK;
+}
+
+int vap_stream_reset(vap_stream* s, void* stream) {
+  if (!s) return fail(VAP_ERR_INVALID, "null stream");
+  return stream_zero(s, (hipStream_t)stream);
+}
+
+void vap_stream_destroy(vap_stream* s) { delete s; }
 
 int vap_encode(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* out, void* workspace,
                size_t workspace_bytes, void* stream) {

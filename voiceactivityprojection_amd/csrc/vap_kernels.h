@@ -116,6 +116,7 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
 hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CONV01_STAMPS=1)
 hipError_t read_rowpanel_stamps(unsigned long long* out);  // diagnostics (VAP_RP_STAMPS=1)
 hipError_t read_ffn_stamps(unsigned long long* out);  // diagnostics (VAP_FFN_STAMPS=1)
+hipError_t read_gemm2_stamps(unsigned long long* out);  // diagnostics (VAP_GEMM2_STAMPS=1)
 
 // Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
 // amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).

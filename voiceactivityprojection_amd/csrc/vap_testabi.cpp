@@ -149,5 +149,6 @@ int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* g
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
+int vap_test_read_gemm_stamps(unsigned long long* out) { return rc_of(read_gemm2_stamps(out)); }
 
 }  // extern "C"

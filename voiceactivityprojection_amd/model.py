@@ -308,6 +308,17 @@ class VapGPT(nn.Module):
         return out
 
 
+def _stream(self, batch: int, context_time: float = 10.0, hop_time: float = 1.0, **kw):
+    """Rolling-window streaming (sds/run_sds.py:206-241; SURVEY config C5): see
+    :class:`voiceactivityprojection_amd.stream.VapStream`."""
+    from .stream import VapStream
+
+    return VapStream(self, batch, context_time=context_time, hop_time=hop_time, **kw)
+
+
+VapGPT.stream = _stream
+
+
 class VAPModel(VapGPT):
     """Inference alias for the reference's ``vap.train.VAPModel`` (vap/train.py:244): a VapGPT."""
 
