@@ -171,6 +171,8 @@ int vap_test_read_rp_stamps(unsigned long long* out);
 int vap_test_read_ffn_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 2 x 4 x 6 s_memtime stamps of sampled bf16 GEMM k-steps (VAP_GEMM2_STAMPS=1) */
 int vap_test_read_gemm_stamps(unsigned long long* out);
+/* timing diagnostics: 8 x 4 x 5 s_memtime stamps of bf16 LSTM steps 100..103 (VAP_LSTM_STAMPS=1) */
+int vap_test_read_lstm_stamps(unsigned long long* out);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,8 @@
 // same lane/register of four accumulator tiles, so the cell update is purely lane-local.
 // h_{t-1} is exchanged through a padded LDS image (one barrier per step); W_hh is pre-packed in
 // MFMA-fragment order so every wave-load is one contiguous KiB.
+#include <cstdlib>
+
 #include "vap_common.h"
 #include "vap_kernels.h"
 
@@ -211,7 +213,13 @@ VAP_DEV void kstep(LstmState& st, const KPre& cur, KPre& nxt, const bf16* gt, co
   if constexpr (UT > 0) {
     if constexpr (KG == 1)  // consumers of the previous tile stay below this point (no MFMA->VALU hazard)
       asm volatile("" : "+v"(st.prev[0]), "+v"(st.prev[1]), "+v"(st.prev[2]), "+v"(st.prev[3]));
-    if constexpr (KG & 1) lstm_cell(st.prev, KG >> 1, st.c[UT - 1][KG >> 1], st.hv[UT - 1][KG >> 1]);
+    if constexpr (KG & 1) {
+      lstm_cell(st.prev, KG >> 1, st.c[UT - 1][KG >> 1], st.hv[UT - 1][KG >> 1]);
+      // pin the cell here, between this k-step's MFMAs and the next's (all volatile asm): left
+      // alone the compiler sinks every cell update to the h write after the step's MFMAs, so the
+      // transcendental work never overlaps the matrix pipe
+      asm volatile("" : "+v"(st.c[UT - 1][KG >> 1]), "+v"(st.hv[UT - 1][KG >> 1]));
+    }
   }
   if constexpr (KG == 7) {
 #pragma unroll
@@ -230,6 +238,11 @@ VAP_DEV void ksteps(LstmState& st, KPre& cur, KPre& nxt, const bf16* gt, const c
   if constexpr (Q + 1 < 32) ksteps<Q + 1>(st, nxt, cur, gt, wa, wv, wl, hb, sl, lane);
 }
 
+// diagnostics (VAP_LSTM_STAMPS=1): wave 0 of workgroups 0..7 records s_memtime at steps 100..103:
+// [step start, k-steps + cell done, after barrier 1, h written, after barrier 2]
+__device__ unsigned long long g_lstm_stamps[8][4][5];
+
+template <bool ST>
 __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __restrict__ gx, int S, int Tn,
                                                               const chunk16* __restrict__ wp, bf16* __restrict__ out,
                                                               int64_t out_seq_stride, LstmSync sync) {
@@ -285,20 +298,35 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
     for (int r = 0; r < 4; ++r) st.c[ut][r] = 0.f;
 
   const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + 64 * w + (lane >> 4) * 4;
+  const int goff = sync.gx_off;
+  auto grow = [&](int t) -> int64_t {  // gate row of step t (a ring when gx_off != 0)
+    const int r = t + goff;
+    return (int64_t)(r >= Tn ? r - Tn : r) * G4;
+  };
 #pragma unroll
   for (int ut = 0; ut < 4; ++ut)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) st.gn[ut][g] = *(const bf16x4*)(gxs + g * HD + ut * 16);
+    for (int g = 0; g < 4; ++g) st.gn[ut][g] = *(const bf16x4*)(gxs + grow(0) + g * HD + ut * 16);
   __syncthreads();
 
   KPre pa, pb;
   int chunk = 0;
+  const bool samp = ST && blockIdx.x < 8 && tid == 0;
+  auto stamp = [&](int t, int k) {
+    if constexpr (ST) {
+      const unsigned long long v = __builtin_amdgcn_s_memtime();
+      if (samp && t >= 100 && t < 104) g_lstm_stamps[blockIdx.x][t - 100][k] = v;
+    }
+  };
   for (int t = 0; t < Tn; ++t) {
-    const bf16* gt = gxs + (int64_t)(t + 1 < Tn ? t + 1 : t) * G4;
+    const bf16* gt = gxs + grow(t + 1 < Tn ? t + 1 : t);
+    stamp(t, 0);
     kload<0>(pa, wl, hb, sl, lane);
     ksteps<0>(st, pa, pb, gt, wa, wv, wl, hb, sl, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(t, 1);
     __builtin_amdgcn_s_barrier();  // every wave has consumed h_{t-1} (no vmcnt drain: gx prefetch stays in flight)
+    stamp(t, 2);
 #pragma unroll
     for (int ut = 0; ut < 4; ++ut) {
       const int u = 64 * w + 16 * ut + (lane >> 4) * 4;
@@ -307,7 +335,9 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
       if (valid) *(bf16x4*)(out + (int64_t)seq * out_seq_stride + (int64_t)t * HD + u) = hv4;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(t, 3);
     __builtin_amdgcn_s_barrier();  // h_t visible to every wave
+    stamp(t, 4);
     if (sync.time_mode && chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) {
       // end of a time chunk: publish its h rows (every chunk ending here), then wait for the next
       // chunk's gate projection
@@ -332,7 +362,7 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
       if (chunk < sync.nr) {
         __syncthreads();
         // the in-step prefetch of step t+1 may predate the projection: load it again
-        const bf16* gn1 = gxs + (int64_t)(t + 1) * G4;
+        const bf16* gn1 = gxs + grow(t + 1);
 #pragma unroll
         for (int ut = 0; ut < 4; ++ut)
 #pragma unroll
@@ -389,9 +419,15 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
       return hipErrorInvalidValue;
     for (int c = 1; c < sync->nr; ++c)
       if (sync->seq_end[c] <= sync->seq_end[c - 1]) return hipErrorInvalidValue;
+    if (sync->gx_off < 0 || sync->gx_off >= Tn) return hipErrorInvalidValue;
     sy = *sync;
   }
-  hipLaunchKernelGGL(lstm_resident_kernel, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
+  static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
+  if (stamps)
+    hipLaunchKernelGGL(lstm_resident_kernel<true>, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
+                     (const chunk16*)whh_packed, out, out_seq_stride, sy);
+  else
+    hipLaunchKernelGGL(lstm_resident_kernel<false>, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
                      (const chunk16*)whh_packed, out, out_seq_stride, sy);
   return hipGetLastError();
 }
@@ -404,3 +440,8 @@ template hipError_t launch_lstm<float>(const float*, int, int, const float*, flo
 template hipError_t launch_lstm<bf16>(const float*, int, int, const bf16*, bf16*, int64_t, hipStream_t);
 template hipError_t launch_pack_whh<float>(const float*, float*, hipStream_t);
 template hipError_t launch_pack_whh<bf16>(const float*, bf16*, hipStream_t);
+
+// diagnostics: copy the LSTM step stamps (8 workgroups x 4 steps x 5) to host memory
+hipError_t read_lstm_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_stamps), sizeof(g_lstm_stamps), 0, hipMemcpyDeviceToHost);
+}

@@ -896,8 +896,9 @@ TcSched tc_schedule(const vap_handle* h, const Plan& p) {
 // The recurrence of the time-chunked forward: ONE persistent launch on a side stream covers every
 // sequence, waiting at each chunk boundary for ready[c] and publishing done[c].
 int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* GX, unsigned char* ws, LstmSync& sy,
-                   hipStream_t st) {
+                   hipStream_t st, int gx_off = 0) {
   sy = LstmSync{};
+  sy.gx_off = gx_off;
   sy.ready = h->sync_mem;
   sy.done = h->sync_mem + vap_handle::MAXMB;
   sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
@@ -967,7 +968,7 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
 // (k4 s2 p1 layers: rows [a, b) need input rows [2a-1, 2b+1) clipped to the layer; conv1 rows come
 // from the fused conv0->conv1 kernel straight from the waveform), then their LSTM gate projections.
 int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigned char* ws, bf16* GX, int64_t a4,
-              int64_t b4, hipStream_t st) {
+              int64_t b4, hipStream_t st, int64_t gx_off = 0) {
   using T = bf16;
   const int S = p.S;
   const int64_t* L = p.L;
@@ -999,9 +1000,15 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
     HIPCHK(gemm<T>(ga, st, false));
   }
+  // gate projections of rows [a4, b4) into ring slots (r + gx_off) mod L4: at most two pieces
   Timed tm(h, VAP_K_LSTM_PROJ, st);
-  HIPCHK(gemm<T>(gargs(Xs[3] + D + a4 * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)(b4 - a4),
-                       S, GX + a4 * 4 * D, 4 * D, L[4] * 4 * D), st, false));
+  for (int64_t r = a4; r < b4;) {
+    const int64_t slot = (r + gx_off) % L[4];
+    const int64_t n = std::min(b4 - r, L[4] - slot);
+    HIPCHK(gemm<T>(gargs(Xs[3] + D + r * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)n, S,
+                         GX + slot * 4 * D, 4 * D, L[4] * 4 * D), st, false));
+    r += n;
+  }
   return VAP_OK;
 }
 
@@ -1176,17 +1183,16 @@ struct vap_stream {
   Plan p;
   unsigned char* ws = nullptr;
   float* win[2] = {};
-  bf16* gx[2] = {};
+  bf16* gx = nullptr;  // gate projections of the window: a ring, row r of the window in slot (r + gx_off) mod L4
+  int64_t gx_off = 0;
   int cur = 0;
   int64_t pushes = 0;
   int64_t keep0 = 0, keep1 = 0;  // conv4 rows [keep0, keep1) carried over from the previous window
   bool reuse = false;
   ~vap_stream() {
     (void)hipFree(ws);
-    for (int i = 0; i < 2; ++i) {
-      (void)hipFree(win[i]);
-      (void)hipFree(gx[i]);
-    }
+    for (int i = 0; i < 2; ++i) (void)hipFree(win[i]);
+    (void)hipFree(gx);
   }
 };
 
@@ -1213,22 +1219,36 @@ int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad
     ++s->pushes;
     return VAP_OK;
   }
-  bf16* GX = s->gx[nxt];
+  bf16* GX = s->gx;
+  // the window moved by hop_rows conv4 rows: carried rows keep their ring slots
+  const int64_t off = s->pushes > 0 ? (s->gx_off + s->hop_rows) % L4 : 0;
   const TcSched t = tc_schedule(h, p);
   LstmSync sy;
-  if ((rc = tc_launch_lstm(h, p, t, GX, s->ws, sy, st))) return rc;
+  if ((rc = tc_launch_lstm(h, p, t, GX, s->ws, sy, st, (int)off))) return rc;
+  int published = 0;
+  auto publish = [&](int64_t rows_ready) -> int {  // ready[c] for every chunk whose steps are all available
+    while (published < t.nch && t.seq_end[published] <= rows_ready)
+      HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published++), sy.epoch, 0));
+    return VAP_OK;
+  };
   if (s->pushes > 0 && s->keep1 > s->keep0) {
-    // carried-over gate projections: new row r = old row r + hop_rows
-    const size_t row = 4 * D * sizeof(bf16);
-    HIPCHK(hipMemcpy2DAsync(GX + s->keep0 * 4 * D, L4 * row, s->gx[s->cur] + (s->keep0 + s->hop_rows) * 4 * D, L4 * row,
-                            (s->keep1 - s->keep0) * row, S, hipMemcpyDeviceToDevice, st));
-    if (s->keep0 > 0 && (rc = conv_rows(h, p, wav, W, s->ws, GX, 0, s->keep0, st))) return rc;
-    if ((rc = conv_rows(h, p, wav, W, s->ws, GX, s->keep1, L4, st))) return rc;
-  } else if ((rc = conv_rows(h, p, wav, W, s->ws, GX, 0, L4, st))) {
-    return rc;
+    // carried-over gate projections (new row r = old row r + hop_rows) stay in their ring slots;
+    // the recurrence starts on them (and the recomputed first row) while the new audio's rows go
+    // through the conv stack
+    if (s->keep0 > 0 && (rc = conv_rows(h, p, wav, W, s->ws, GX, 0, s->keep0, st, off))) return rc;
+    if ((rc = publish(s->keep1))) return rc;
+    if ((rc = conv_rows(h, p, wav, W, s->ws, GX, s->keep1, L4, st, off))) return rc;
+  } else {
+    int64_t done = 0;  // first push: the front end chunk by chunk, as run_forward_tc
+    for (int c = 0; c < t.nch; ++c) {
+      if ((rc = conv_rows(h, p, wav, W, s->ws, GX, done, t.seq_end[c], st, off))) return rc;
+      done = t.seq_end[c];
+      if ((rc = publish(done))) return rc;
+    }
   }
-  for (int c = 0; c < t.nch; ++c) HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
+  if ((rc = publish(L4))) return rc;
   if ((rc = tc_back_end(h, p, t, sy, s->ws, logits, vadl, st))) return rc;
+  s->gx_off = off;
   s->cur = nxt;
   ++s->pushes;
   return VAP_OK;
@@ -1395,8 +1415,7 @@ int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t 
   s->reuse = bf && h->use_time_chunks() && h->wait_value && hop_samples % 160 == 0;
   if (const char* e = getenv("VAP_STREAM_REUSE")) s->reuse = s->reuse && atoi(e) != 0;  // A/B: 0 = recompute
   if (s->reuse) {
-    for (int i = 0; i < 2; ++i)
-      if (hipMalloc(&s->gx[i], (size_t)S * L[4] * 4 * D * sizeof(bf16)) != hipSuccess) return bail("gate buffers");
+    if (hipMalloc(&s->gx, (size_t)S * L[4] * 4 * D * sizeof(bf16)) != hipSuccess) return bail("gate buffer");
     s->hop_rows = (int)(hop_samples / 160);
     int64_t c0 = 0;
     while (c0 < L[4] && !conv4_row_clean(L, window_samples, c0)) ++c0;

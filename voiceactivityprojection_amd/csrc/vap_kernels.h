@@ -64,6 +64,7 @@ struct LstmSync {
                      // time chunk: every workgroup waits ready[c] before the chunk and adds 1 to
                      // done[c] after it)
   int time_mode;
+  int gx_off = 0;    // gate rows form a ring: step t reads gx row (t + gx_off) mod Tn (streaming)
 };
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
                                 int64_t out_seq_stride, hipStream_t st, const LstmSync* sync);
@@ -117,6 +118,7 @@ hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CON
 hipError_t read_rowpanel_stamps(unsigned long long* out);  // diagnostics (VAP_RP_STAMPS=1)
 hipError_t read_ffn_stamps(unsigned long long* out);  // diagnostics (VAP_FFN_STAMPS=1)
 hipError_t read_gemm2_stamps(unsigned long long* out);  // diagnostics (VAP_GEMM2_STAMPS=1)
+hipError_t read_lstm_stamps(unsigned long long* out);  // diagnostics (VAP_LSTM_STAMPS=1)
 
 // Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
 // amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).

@@ -150,5 +150,6 @@ int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_sta
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
 int vap_test_read_gemm_stamps(unsigned long long* out) { return rc_of(read_gemm2_stamps(out)); }
+int vap_test_read_lstm_stamps(unsigned long long* out) { return rc_of(read_lstm_stamps(out)); }
 
 }  // extern "C"
