@@ -32,11 +32,17 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros((8, 24), dtype=np.uint64)
     N.check(N.lib().vap_test_read_stamps(ctypes.c_void_p(buf.ctypes.data)))
-    names = ["prologue"] + [f"p{r}_{x}" for r in range(4) for x in ("sv", "g", "ksteps")] + ["epilogue"]
+    if not any(os.environ.get(f"VAP_CONV01_V{v}") for v in (2, 4)):
+        # v5: start | prologue | units 0-7, 8-15, 16-23, 24-31 | epilogue
+        names, n = ["prologue", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 7
+    elif os.environ.get("VAP_CONV01_V4"):  # v4: start | prologue | units 0-7, 8-15, 16-23, 24-31 | epilogue
+        names, n = ["prologue", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 7
+    else:
+        names, n = ["prologue"] + [f"p{r}_{x}" for r in range(4) for x in ("sv", "g", "ksteps")] + ["epilogue"], 14
     for i in range(8):
         st = buf[i].astype(np.int64)
-        d = np.diff(st[:14])
-        print(f"wg{i}: total {st[13] - st[0]:7d} | " + " ".join(f"{n}={v}" for n, v in zip(names, d)))
+        d = np.diff(st[:n])
+        print(f"wg{i}: total {st[n - 1] - st[0]:7d} | " + " ".join(f"{k}={v}" for k, v in zip(names, d)))
 
 
 if __name__ == "__main__":

@@ -9,7 +9,9 @@
 // phase r, the needed positions are G_r[i] = x0[4(t0+i) - 2 + r], i = 0..128, and output row i uses
 // G_r[i] (h = 0) and G_r[i+1] (h = 1).  Per phase the workgroup regenerates G_r (129 x 256 bf16) in
 // LDS and runs the 512-deep K slice (taps r and r+4) of the conv1 GEMM against W1 tiles streamed
-// from L2.  Every conv0 position is generated once per tile (plus one halo row per phase).
+// from L2.  Every conv0 position is generated once per tile (plus one halo row per phase).  That is
+// the v2 kernel below (VAP_CONV01_V2=1); the default v9 kernel makes the same image in 32-channel
+// slices inside the MFMA stream on 256-row tiles (see its header).
 //
 // conv0 itself runs on the MFMA: z^T[c][p] = sum_k A[c][k] S[k][p] with a K = 32 split-bf16 layout
 //   k  0..9 : A = w_hi[c],  S = s_hi[p]      k 10..19: A = w_hi[c], S = s_lo[p]
@@ -19,6 +21,7 @@
 // rstd_p comes from the exact centred quadratic form  var = (s^T G s + 2 h.s + beta)/255,
 // G = Wc^T Wc (10x10), h = Wc^T bc, beta = bc.bc  (Wc, bc = centred conv0 weights / bias), so the
 // statistics need no pass over the 256 channels.  Padding positions (p < 0 or p >= L0) are zero rows.
+#include <algorithm>
 #include <cstdlib>
 
 #include "vap_common.h"
@@ -51,236 +54,8 @@ struct C0Stat {  // layout of the c0stat float array (host-computed at weight pa
   static constexpr int N = 112;
 };
 
-__global__ __launch_bounds__(512) void conv01_kernel(const float* __restrict__ wav, int64_t N, int L0, int L1,
-                                                    const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
-                                                    const float* __restrict__ beta0, const bf16* __restrict__ W1,
-                                                    const float* __restrict__ b1, const float* __restrict__ g1,
-                                                    const float* __restrict__ be1, bf16* __restrict__ out,
-                                                    int64_t out_seq_stride, int r0, int r1) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
-  unsigned char* G = smem + OFF_G;
-  unsigned char* Bt = smem + OFF_B;
-  unsigned char* SV = smem + OFF_SV;
-  float* RS = (float*)(smem + OFF_RS);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1;
-  const int s = blockIdx.y;
-  const int t0 = r0 + blockIdx.x * BM;  // output rows [r0, r1) of conv1
-  const float* src = wav + (int64_t)s * N;
-
-  // conv0 A fragments of this wave: channel tiles 2w, 2w+1 (row c, k = 8(lane>>4)..+7)
-  chunk16 a0f[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) a0f[j] = c0w[((2 * w + j) * 16 + (lane & 15)) * 4 + (lane >> 4)];
-  float bet[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bet[j][e] = beta0[(2 * w + j) * 16 + 4 * (lane >> 4) + e];
-
-  // W1 staging: 2048 chunks of 16 B per k-step (256 rows x 8), 4 per thread
-  const bf16* bptr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int id = tid + i * 512, row = id >> 3, c = id & 7;
-    bptr[i] = W1 + (int64_t)row * 2048 + c * 8;
-  }
-  chunk16 rb[4];
-  auto kbase = [](int q) {  // global k-step q (0..31): phase r = q>>3, half h = (q>>2)&1, sub (q&3)
-    const int r = q >> 3, hh = (q >> 2) & 1, kk = q & 3;
-    return (r + 4 * hh) * 256 + kk * 64;
-  };
-  auto gload = [&](int q) {
-    const int kb = kbase(q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + kb);
-  };
-  auto lstore = [&](int buf) {
-    unsigned char* base = Bt + buf * BN * BROWB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + i * 512, row = id >> 3, c = id & 7;
-      *(chunk16*)(base + row * BROWB + bswz(row, c) * 16) = rb[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  gload(0);
-  for (int r = 0; r < 4; ++r) {
-    // ---------------- (a) split sample vectors + ChannelNorm statistics for the phase positions
-    if (tid < NPOS) {
-      const int i = tid;
-      const int p = 4 * (t0 + i) - 2 + r;
-      const bool valid = i < GROWS && p >= 0 && p < L0;
-      float sm[10];
-      const int64_t i0 = (int64_t)p * 5 - 3;
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int64_t ix = i0 + k;
-        sm[k] = (valid && ix >= 0 && ix < N) ? src[ix] : 0.f;
-      }
-      bf16 hi[10], lo[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        hi[k] = (bf16)sm[k];
-        lo[k] = (bf16)(sm[k] - (float)hi[k]);
-      }
-      bf16x8 v0 = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
-      bf16x8 v1 = {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]};
-      bf16x8 v2 = {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]};
-      bf16x8 v3 = {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], (bf16)1.0f, (bf16)1.0f};
-      unsigned char* row = SV + i * SVROW;
-      *(bf16x8*)(row + 0) = v0;
-      *(bf16x8*)(row + 16) = v1;
-      *(bf16x8*)(row + 32) = v2;
-      *(bf16x8*)(row + 48) = v3;
-      // var * 255 = s^T G s + 2 h.s + beta  (centred, exact in exact arithmetic)
-      float q = c0stat[C0Stat::BETA];
-#pragma unroll
-      for (int a = 0; a < 10; ++a) {
-        float ga = 2.0f * c0stat[C0Stat::H + a];
-#pragma unroll
-        for (int b = 0; b < 10; ++b) ga = fmaf(c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
-        q = fmaf(ga, sm[a], q);
-      }
-      RS[i] = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : -1.0f;
-    }
-    __syncthreads();  // (also: every wave finished reading the previous phase's G)
-
-    // ---------------- (b) conv0 on the MFMA -> ChannelNorm/ReLU -> bf16 G image
-#pragma unroll
-    for (int pt = 0; pt < NPOS / 16; ++pt) {
-      const int prow = pt * 16 + (lane & 15);  // position row of this lane's column
-      const chunk16 bfr = *(const chunk16*)(SV + prow * SVROW + (lane >> 4) * 16);
-      const float rs = RS[prow];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        z = mfma_chunk<bf16>(a0f[j], bfr, z);
-        if (prow < GROWS) {
-          const int c = (2 * w + j) * 16 + 4 * (lane >> 4);  // 4 consecutive channels
-          bf16x4 o4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o4[e] = (bf16)(rs < 0.f ? 0.f : fmaxf(fmaf(rs, z[e], bet[j][e]), 0.f));
-          *(bf16x4*)(G + prow * GROWB + gswz(prow, c >> 3) * 16 + (c & 7) * 2) = o4;
-        }
-      }
-    }
-    // stage the first W1 tile of this phase
-    lstore(0);
-    __syncthreads();
-
-    // ---------------- (c) 8 k-steps of 64 over taps r (h = 0) and r + 4 (h = 1)
-    for (int kq = 0; kq < 8; ++kq) {
-      const int q = r * 8 + kq;
-      const int cur = kq & 1;
-      if (q + 1 < 32) gload(q + 1);
-      const int hh = kq >> 2, kk = kq & 3;
-      const unsigned char* bbase = Bt + cur * BN * BROWB;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        chunk16 af[4], bfr[4];
-        const int c16 = kk * 8 + sub * 4 + (lane >> 4);  // chunk within the 512-B G row
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = wm * 64 + i * 16 + (lane & 15) + hh;
-          af[i] = *(const chunk16*)(G + row * GROWB + gswz(row, c16) * 16);
-        }
-        const int cb = sub * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = wn * 64 + j * 16 + (lane & 15);
-          bfr[j] = *(const chunk16*)(bbase + row * BROWB + bswz(row, cb) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<bf16>(af[i], bfr[j], acc[i][j]);
-      }
-      if (kq + 1 < 8) lstore(cur ^ 1);
-      __syncthreads();
-    }
-  }
-
-  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  const int colb = wn * 64 + (lane & 15);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float b = b1[colb + j * 16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i][j] += b;
-  }
-  float* red = (float*)Bt;  // [BM][4]
-  float mean[4][4], rstd[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float sum = acc[i][0][e] + acc[i][1][e] + acc[i][2][e] + acc[i][3][e];
-      sum += __shfl_xor(sum, 1, 64);
-      sum += __shfl_xor(sum, 2, 64);
-      sum += __shfl_xor(sum, 4, 64);
-      sum += __shfl_xor(sum, 8, 64);
-      if ((lane & 15) == 0) red[(wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4 + wn] = sum;
-    }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4);
-      mean[i][e] = (pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / BN);
-    }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = acc[i][j][e] - mean[i][e];
-        ss += d * d;
-      }
-      ss += __shfl_xor(ss, 1, 64);
-      ss += __shfl_xor(ss, 2, 64);
-      ss += __shfl_xor(ss, 4, 64);
-      ss += __shfl_xor(ss, 8, 64);
-      if ((lane & 15) == 0) red[(wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4 + wn] = ss;
-    }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane >> 4) * 4 + e) * 4);
-      rstd[i][e] = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
-    }
-  bf16* obase = out + (int64_t)s * out_seq_stride;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int t = t0 + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
-      if (t >= r1) continue;
-      bf16* orow = obase + (int64_t)t * BN;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = colb + j * 16;
-        const float v = (acc[i][j][e] - mean[i][e]) * rstd[i][e] * g1[col] + be1[col];
-        orow[col] = (bf16)fmaxf(v, 0.f);
-      }
-    }
-}
-
 // ------------------------------------------------------------------------------------------
-// v2 (default): the same fused math, restaged for the MI355X memory pipeline:
+// v2 (VAP_CONV01_V2=1): the same fused math, restaged for the MI355X memory pipeline:
 //   * W1 k-tiles (256 rows x 64 k) arrive by LDS-DMA (global_load_lds_dwordx4, swizzle applied to
 //     the source address), two stages, raw s_barrier + vmcnt: the next tile's DMA stays in flight
 //     across the MFMAs, the phase barriers and the conv0 regeneration;
@@ -362,14 +137,15 @@ __global__ __launch_bounds__(512, 1) void conv01b_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (w * 2 + i) * 16 + (lane >> 2);
-    woff[i] = (uint32_t)(row * 2048 + wswz(row, lane & 3) * 8) * 2;
+    woff[i] = (uint32_t)(row * 64 + wswz(row, lane & 3) * 16);
   }
-  auto kbase = [](int q) {  // k-step q (0..63): phase q>>4, tap half (q>>3)&1, 32-channel group q&7
-    return ((q >> 4) + 4 * ((q >> 3) & 1)) * 256 + (q & 7) * 32;
+  // W1 in the k-step-major layout [K/32][256][32] (launch_pack_kstep): one stage = 16 KiB contiguous
+  auto kstep_of = [](int q) {  // k-step q (0..63): phase q>>4, tap half (q>>3)&1, 32-channel group q&7
+    return ((q >> 4) + 4 * ((q >> 3) & 1)) * 8 + (q & 7);
   };
   auto dma = [&](int q) {
     unsigned char* base = Wt + (q & 3) * WST;
-    const uint32_t kb = (uint32_t)kbase(q) * 2;
+    const uint32_t kb = (uint32_t)kstep_of(q) * 16384;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(W1b + (woff[i] + kb)), (lds_void_t*)(base + (w * 2 + i) * 1024), 16, 0, 0);
@@ -565,269 +341,444 @@ __global__ __launch_bounds__(512, 1) void conv01b_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// v3 (default): v2's staging with 4 waves (one per SIMD) of 64 rows x 128 channels each: per
-// 32-deep step a wave reads 4 G + 8 W1 fragments for 32 MFMAs (v2: 4 + 4 for 16), halving the LDS
-// read traffic per MFMA -- the G reads are inherently 2-way bank conflicted (the tap-shifted row
-// offset), so LDS, not the MFMA pipe, bounded v2.
-// v2: the same fused math, restaged for the MI355X memory pipeline:
-//   * W1 k-tiles (256 rows x 64 k) arrive by LDS-DMA (global_load_lds_dwordx4, swizzle applied to
-//     the source address), two stages, raw s_barrier + vmcnt: the next tile's DMA stays in flight
-//     across the MFMAs, the phase barriers and the conv0 regeneration;
-//   * the tile's whole waveform segment (~10 KiB, every phase's samples) is loaded into LDS once, so
-//     a phase's split samples / ChannelNorm statistics come from LDS instead of dependent global loads;
-//   * operands swapped (C^T = W1 G^T): a lane owns 4 consecutive output channels of one row ->
-//     8-byte bf16 stores (16 per lane instead of 64 two-byte stores), ChannelNorm row statistics by a
-//     16-lane-stride shuffle + LDS.
+// Shared pieces of the slice-pipelined kernel (v9)
 // ------------------------------------------------------------------------------------------
+VAP_DEV int sphys(int row, int c) { return (c + 2 * (row >> 2)) & 3; }  // 64-B slice / SV rows
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+VAP_DEV uint32_t relu_bf16x2(float a, float b) {  // bf16(max(x, 0)) for two values: cvt_pk + pk_max_i16
+  const bf16x2_t h = __builtin_convertvector((f32x2){a, b}, bf16x2_t);
+  s16x2 v = __builtin_bit_cast(s16x2, h);
+  v = __builtin_elementwise_max(v, (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
+VAP_DEV void mfma_acc(f32x4& c, const chunk16& a, const chunk16& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+constexpr int BM2 = 256, NPOS2 = 272, GROWS2 = BM2 + 1;        // 17 position tiles of 16 (>= 257)
+constexpr int WSEG2 = 20 * BM2 + 32;                            // 5152 waveform floats per tile
+constexpr int I_SVN = 4 * NPOS2;                                // 1088 split-sample rows
+constexpr int I_GSLOT = NPOS2 * 64;                             // 17408
 
+// ------------------------------------------------------------------------------------------
+// v9 (default): the conv0 image in (phase, 32-channel) SLICES on 256-row tiles, four waves.
+// conv1's K for phase r is taps r and r+4 over 256 channels.  Ordered as units u = (r = u>>3,
+// g = u&7) of one 32-channel group with both taps (two 32-deep k-steps), a unit needs only the slice
+// G_r[:, 32g..+32) (257 rows x 64 B).  ChannelNorm-0 statistics are per position and closed-form,
+// so a slice is independent of the other channels and is made two units ahead, inside the MFMA
+// stream, instead of regenerating a whole-phase image between k-loops (v2: 27 % of a tile).
+//   * a wave owns 256 rows x 64 output channels: 64 MFMAs per k-step on 16 G + 4 W1 fragments, the
+//     256 accumulators in AGPRs (inline-asm MFMA with "+a"); no two waves share a W1 fragment, so
+//     W1 goes straight from L2 into VGPRs (k-step-major layout: one fragment = 1 KiB contiguous) --
+//     at 256 rows per tile the W1 stream is 16 B / cycle / CU, within what L2 sustains;
+//   * ChannelNorm-0 folded into the conv0 operand: the prologue stores rstd_p * [s_hi | s_lo | s_hi |
+//     1 1] (split-bf16 after scaling) and the conv0 MFMA starts from beta0, so a slice is
+//     relu(MFMA) -> bf16 (v_pk_max_i16 on the packed bit patterns) with no per-position loads;
+//   * three slice slots (slice v in slot v%3): slice u+2 is made during unit u into the slot of
+//     slice u-1, so ONE barrier at the start of unit u publishes slice u+1 and frees that slot, and
+//     the G fragments are read just in time (3 MFMA groups ahead through a 4-register ring) instead
+//     of a whole k-step ahead -- which frees the VGPRs for
+//   * a three-set W1 register ring: unit u+2's fragments load at the start of unit u (64 KiB in
+//     flight per CU, two units of latency budget);
+//   * the slice work has no branches: every wave makes position tile 16 (the rows 256.. that only
+//     output row 255 reads), padding positions are zeroed with a per-lane validity mask, and slices
+//     past the last unit go to slots nothing reads.
+// The waveform segment (prologue only) shares its LDS with slot 2 and the epilogue's reduction area.
+// Stamps (VAP_CONV01_STAMPS, tools/stamps_conv01.py; 256-row tile): prologue 17k, 32 units 108k
+// (3.4k per unit against 2,048 cycles of MFMA: +0.4k W1 loads, +1k slice work), epilogue 22k.
+// ------------------------------------------------------------------------------------------
+constexpr int J_OFF_G = 0;                                    // 3 slots of 272 x 64 B
+constexpr int J_OFF_RED = J_OFF_G + 3 * I_GSLOT;              // 52224 (epilogue)
+constexpr int J_OFF_WV = J_OFF_G + 2 * I_GSLOT;               // 34816: over slot 2 + red (prologue)
+constexpr int J_OFF_SV = J_OFF_RED + BM2 * 4 * 4;             // 56320
+constexpr int J_OFF_C0 = J_OFF_SV + I_SVN * 64;               // 125952
+constexpr int J_OFF_BE = J_OFF_C0 + 256 * 64;                 // 142336
+constexpr int J_LDS = J_OFF_BE + 4 * 256 * 4;                 // 146432
+static_assert(J_OFF_WV + WSEG2 * 4 <= J_OFF_SV, "conv01 v9 waveform alias");
+static_assert(J_LDS <= 163840, "conv01 v9 LDS");
 
-
-__global__ __launch_bounds__(256, 1) void conv01c_kernel(const float* __restrict__ wav, int64_t N, int L0,
+template <bool STAMPS, int DIAG = 0>
+__global__ __launch_bounds__(256, 1) void conv01i_kernel(const float* __restrict__ wav, int64_t N, int L0,
                                                         const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
                                                         const float* __restrict__ beta0, const bf16* __restrict__ W1,
                                                         const float* __restrict__ b1, const float* __restrict__ g1,
                                                         const float* __restrict__ be1, bf16* __restrict__ out,
                                                         int64_t out_seq_stride, int r0, int r1) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[B_LDS];
-  unsigned char* G = smem + B_OFF_G;
-  unsigned char* Wt = smem + B_OFF_W;
-  unsigned char* SV = smem + B_OFF_SV;
-  float* RS = (float*)(smem + B_OFF_RS);
-  float* WV = (float*)(smem + B_OFF_WV);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[J_LDS];
+  unsigned char* G = smem + J_OFF_G;
+  unsigned char* SV = smem + J_OFF_SV;
+  unsigned char* C0 = smem + J_OFF_C0;
+  float* BE = (float*)(smem + J_OFF_BE);
+  float* EP = BE + 256;
+  float* WV = (float*)(smem + J_OFF_WV);
+  float* red = (float*)(smem + J_OFF_RED);
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1;  // 64 rows (t) x 128 output channels per wave
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 64w..64w+63, all 256 rows
   const int s = blockIdx.y;
-  const int t0 = r0 + blockIdx.x * BM;
-  const float* src = wav + (int64_t)s * N;
-  const unsigned char* W1b = (const unsigned char*)W1;
+  const int t0 = r0 + blockIdx.x * BM2;
 
-  // W1 DMA: a piece = 8 rows x 128 B; wave w fills pieces 8w..8w+7 of a 32-piece stage; lane ->
-  // (row 8p + lane/8, physical chunk lane%8) holding logical chunk (lane%8) ^ bswz(row)
-  uint32_t woff[8];
+  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
+  unsigned long long stv[24];
+  int nst = 0;
+  auto stamp = [&]() {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (nst < 24) stv[nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp();
+
+  // W1 fragments by buffer loads: one lane offset VGPR, the k-step / fragment offset in an SGPR
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W1, 64 * 256 * 64);
+  const uint32_t wlo = (uint32_t)(((w * 64 + (lane & 15)) * 4 + (lane >> 4)) * 16);
+  auto wload = [&](int u, chunk16* wf) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (w * 8 + i) * 8 + (lane >> 3);
-    woff[i] = (uint32_t)(row * 2048 + bswz(row, lane & 7) * 8) * 2;
+    for (int h = 0; h < 2; ++h) {
+      const int kk = ((u >> 3) + 4 * h) * 8 + (u & 7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[h * 4 + j] = buf_load16(wrs, wlo, (uint32_t)(kk * 16384 + j * 1024));
+    }
+  };
+
+  // ---------------- prologue
+  {
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(wav + (int64_t)s * N, (uint32_t)(N * 4));
+    const int xb = 20 * t0 - 13;  // first sample of the segment (negative offsets read as zero)
+    uint32_t wv[21];
+#pragma unroll
+    for (int k = 0; k < 21; ++k)
+      wv[k] = __builtin_amdgcn_raw_buffer_load_b32(wr, (int)((uint32_t)(xb + tid + 256 * k) * 4u), 0, 0);
+    chunk16 c0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c0[i] = c0w[tid + i * 256];
+    f32x4 ep;
+    if (tid < 64) ep = ((const f32x4*)beta0)[tid];
+    else if (tid < 128) ep = ((const f32x4*)b1)[tid - 64];
+    else if (tid < 192) ep = ((const f32x4*)g1)[tid - 128];
+    else ep = ((const f32x4*)be1)[tid - 192];
+#pragma unroll
+    for (int k = 0; k < 21; ++k)
+      if (tid + 256 * k < WSEG2) WV[tid + 256 * k] = __builtin_bit_cast(float, wv[k]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ((chunk16*)C0)[tid + i * 256] = c0[i];
+    ((f32x4*)BE)[tid] = ep;
   }
-  auto kbase = [](int q) {  // k-step q (0..31): phase r = q>>3, tap half h = (q>>2)&1, 64-channel group q&3
-    return ((q >> 3) + 4 * ((q >> 2) & 1)) * 256 + (q & 3) * 64;
-  };
-  auto dma = [&](int q) {
-    unsigned char* base = Wt + (q & 1) * BN * BROWB;
-    const uint32_t kb = (uint32_t)kbase(q) * 2;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(W1b + (woff[i] + kb)), (lds_void_t*)(base + (w * 8 + i) * 1024), 16, 0, 0);
-  };
+  chunk16 W[3][8];  // W1 register ring: unit u in set u % 3
+  wload(0, W[0]);
+  wload(1, W[1]);
+  __syncthreads();
 
-  // conv0 operand fragments of this wave (channel tiles 4w..4w+3) and folded ChannelNorm shifts
-  chunk16 a0f[4];
+  for (int j = tid; j < I_SVN; j += 256) {
+    const int r = j / NPOS2, i = j - r * NPOS2;
+    const int p = 4 * (t0 + i) - 2 + r;
+    const bool valid = i < GROWS2 && p >= 0 && p < L0;
+    float sm[10];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) a0f[j] = c0w[((4 * w + j) * 16 + (lane & 15)) * 4 + (lane >> 4)];
-  float bet[4][4];
+    for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG2 - 1)];
+    float q = c0stat[C0Stat::BETA];
+#pragma unroll
+    for (int a = 0; a < 10; ++a) {
+      float ga = fmaf(c0stat[C0Stat::G + a * 10 + a], sm[a], 2.0f * c0stat[C0Stat::H + a]);
+#pragma unroll
+      for (int b = a + 1; b < 10; ++b) ga = fmaf(2.0f * c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
+      q = fmaf(ga, sm[a], q);
+    }
+    const float rs = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : 0.f;
+    bf16 hi[10], lo[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const float x = rs * sm[k];
+      hi[k] = (bf16)x;
+      lo[k] = (bf16)(x - (float)hi[k]);
+    }
+    const bf16 rb = (bf16)rs;
+    const bf16x8 v[4] = {{hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]},
+                         {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]},
+                         {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]},
+                         {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], rb, rb}};
+    unsigned char* row = SV + j * 64;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(bf16x8*)(row + sphys(j, c) * 16) = v[c];
+  }
+
+  // validity of this lane's position in tile x (w, w+4, w+8, w+12, 16) of phase r: bit 5r + x
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      const int pt = x == 4 ? 16 : w + 4 * x;
+      const int p = 4 * (t0 + pt * 16 + (lane & 15)) - 2 + r;
+      vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
+    }
+  __syncthreads();
+
+  // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; rows >= 257 are never read
+  auto read_c0 = [&](int v, chunk16* c0, f32x4* bt) {
+    const int g = v & 7;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      c0[ct] = ((const chunk16*)C0)[((2 * g + ct) * 16 + (lane & 15)) * 4 + (lane >> 4)];
+      bt[ct] = *(const f32x4*)(BE + (2 * g + ct) * 16 + 4 * (lane >> 4));
+    }
+  };
+  auto read_sv = [&](int v, int x) -> chunk16 {
+    const int pt = x == 4 ? 16 : w + 4 * x;
+    const int jj = ((v >> 3) & 3) * NPOS2 + pt * 16 + (lane & 15);
+    return *(const chunk16*)(SV + jj * 64 + sphys(jj, lane >> 4) * 16);
+  };
+  auto pstore = [&](int v, int x, const f32x4* z) {
+    const int pt = x == 4 ? 16 : w + 4 * x;
+    const int prow = pt * 16 + (lane & 15);
+    const uint32_t m = 0u - ((vmask >> (5 * ((v >> 3) & 3) + x)) & 1u);
+    unsigned char* gs = G + (v % 3) * I_GSLOT;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const u32x2 o = {relu_bf16x2(z[ct][0], z[ct][1]) & m, relu_bf16x2(z[ct][2], z[ct][3]) & m};
+      const int lc = 2 * ct + (lane >> 5);
+      if constexpr (DIAG & 16) asm volatile("" ::"v"(o));
+      else *(u32x2*)(gs + prow * 64 + sphys(prow, lc) * 16 + ((lane >> 4) & 1) * 8) = o;
+    }
+  };
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {  // slices 0 and 1
+    chunk16 c0[2];
+    f32x4 bt[2], z[2];
+    read_c0(v, c0, bt);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      const chunk16 sv = read_sv(v, x);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) z[ct] = mfma_chunk<bf16>(c0[ct], sv, bt[ct]);
+      pstore(v, x, z);
+    }
+  }
+
+  f32x4 acc[4][16];  // [n tile][m tile] of C^T, in AGPRs
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bet[j][e] = beta0[(4 * w + j) * 16 + 4 * (lane >> 4) + e];
+    for (int i = 0; i < 16; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // the tile's waveform segment: samples 20*t0 - 13 + [0, WSEG) (zeros outside the signal)
-  const int64_t xb = (int64_t)20 * t0 - 13;
-  for (int i = tid; i < WSEG; i += 256) {
-    const int64_t ix = xb + i;
-    WV[i] = (ix >= 0 && ix < N) ? src[ix] : 0.f;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only the DMA ring uses vmcnt from here on
-  dma(0);
-  lds_barrier();
+  // fragment stream of unit u: n = 16h + i -> k-step (u,h), row block i; reads run 3 groups ahead
+  auto gread = [&](int u, int n) -> chunk16 {
+    const unsigned char* gs = G + (u % 3) * I_GSLOT;
+    const int row = (n & 15) * 16 + (lane & 15) + (n >> 4);
+    return *(const chunk16*)(gs + row * 64 + sphys(row, lane >> 4) * 16);
+  };
+  chunk16 gf[4];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // slices 0, 1 published; WV (slot 2) free
+#pragma unroll
+  for (int n = 0; n < 3; ++n) gf[n] = gread(0, n);
+  stamp();
 
-  f32x4 acc[8][4];  // [n tile][m tile] of C^T
+  auto unit = [&](const int u, chunk16* wf, chunk16* wn2, const bool last1, const bool last2) {
+    // B_u: own slice u+1 stores retired; W1 of unit u landed (unit u+1's 8 loads are younger)
+    __builtin_amdgcn_sched_barrier(0);
+    if (last1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!(DIAG & 4))
+      if (!last2) wload(u + 2, wn2);
+    const int v = u + 2;
+    chunk16 c0[2], sv;
+    f32x4 bt[2], z[2][2];
+    if constexpr (!(DIAG & 2)) read_c0(v, c0, bt);
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int r = 0; r < 4; ++r) {
-    // ---------------- (a) split samples + ChannelNorm statistics of the phase positions (LDS only)
-    if (tid < NPOS) {
-      const int i = tid;
-      const int p = 4 * (t0 + i) - 2 + r;
-      const bool valid = i < GROWS && p >= 0 && p < L0;
-      float sm[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG - 1)];
-      bf16 hi[10], lo[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        hi[k] = (bf16)sm[k];
-        lo[k] = (bf16)(sm[k] - (float)hi[k]);
-      }
-      bf16x8 v0 = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
-      bf16x8 v1 = {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]};
-      bf16x8 v2 = {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]};
-      bf16x8 v3 = {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], (bf16)1.0f, (bf16)1.0f};
-      unsigned char* row = SV + i * SVROW;
-      *(bf16x8*)(row + 0) = v0;
-      *(bf16x8*)(row + 16) = v1;
-      *(bf16x8*)(row + 32) = v2;
-      *(bf16x8*)(row + 48) = v3;
-      float q = c0stat[C0Stat::BETA];
-#pragma unroll
-      for (int a = 0; a < 10; ++a) {
-        float ga = 2.0f * c0stat[C0Stat::H + a];
-#pragma unroll
-        for (int b = 0; b < 10; ++b) ga = fmaf(c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
-        q = fmaf(ga, sm[a], q);
-      }
-      RS[i] = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : -1.0f;
-    }
-    lds_barrier();  // SV/RS ready; every wave done reading the previous phase's G
-
-    // ---------------- (b) conv0 on the MFMA -> ChannelNorm/ReLU -> bf16 G image
-#pragma unroll
-    for (int pt = 0; pt < NPOS / 16; ++pt) {
-      const int prow = pt * 16 + (lane & 15);
-      const chunk16 bfr = *(const chunk16*)(SV + prow * SVROW + (lane >> 4) * 16);
-      const float rs = RS[prow];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        z = mfma_chunk<bf16>(a0f[j], bfr, z);
-        if (prow < GROWS) {
-          const int c = (4 * w + j) * 16 + 4 * (lane >> 4);
-          bf16x4 o4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o4[e] = (bf16)(rs < 0.f ? 0.f : fmaxf(fmaf(rs, z[e], bet[j][e]), 0.f));
-          *(bf16x4*)(G + prow * GROWB + gswz(prow, c >> 3) * 16 + (c & 7) * 2) = o4;
-        }
-      }
-    }
-    lds_barrier();  // G ready
-
-    // ---------------- (c) 8 k-steps of 64 over taps r (h = 0) and r + 4 (h = 1)
-    for (int kq = 0; kq < 8; ++kq) {
-      const int q = r * 8 + kq;
+    for (int n = 0; n < 32; ++n) {
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage q landed
-      __builtin_amdgcn_s_barrier();                       // every wave's; stage q-1's buffer fully read
-      __builtin_amdgcn_sched_barrier(0);
-      if (q + 1 < 32) dma(q + 1);
-      const int hh = kq >> 2, kk = kq & 3;
-      const unsigned char* wb = Wt + (q & 1) * BN * BROWB;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        chunk16 gf[4], wf[8];
-        const int c16 = kk * 8 + sub * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = wm * 64 + i * 16 + (lane & 15) + hh;
-          gf[i] = *(const chunk16*)(G + row * GROWB + gswz(row, c16) * 16);
+      if constexpr (!(DIAG & 2)) {  // slice v: tile x operands at group 6x, MFMAs at 6x+2, stores at 6x+4
+        if (n % 6 == 0 && n / 6 < 5) {
+          if constexpr (DIAG & 64) sv = c0[0];
+          else sv = read_sv(v, n / 6);
         }
-        const int cb = sub * 4 + (lane >> 4);
+        if (n % 6 == 2 && n / 6 < 5)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int row = wn * 128 + j * 16 + (lane & 15);
-          wf[j] = *(const chunk16*)(wb + row * BROWB + bswz(row, cb) * 16);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[j][i] = mfma_chunk<bf16>(wf[j], gf[i], acc[j][i]);
+          for (int ct = 0; ct < 2; ++ct) {
+            if constexpr (DIAG & 32) z[(n / 6) & 1][ct] = bt[ct] + __builtin_bit_cast(f32x4, sv);
+            else z[(n / 6) & 1][ct] = mfma_chunk<bf16>(c0[ct], sv, bt[ct]);
+          }
+        if (n % 6 == 4 && n / 6 < 5) pstore(v, n / 6, z[(n / 6) & 1]);
       }
+      const int i = n & 15, h = n >> 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if constexpr (!(DIAG & 8)) mfma_acc(acc[j][i], wf[4 * h + j], gf[n & 3]);
+      if (n + 3 < 32) gf[(n + 3) & 3] = gread(u, n + 3);
+      else if (!last1) gf[(n + 3) & 3] = gread(u + 1, n + 3 - 32);
     }
+    if ((u & 7) == 7) stamp();
+  };
+  for (int u = 0; u < 30; u += 3) {
+    unit(u, W[0], W[2], false, false);
+    unit(u + 1, W[1], W[0], false, false);
+    unit(u + 2, W[2], W[1], false, u + 2 >= 30);
   }
+  unit(30, W[0], W[2], false, true);
+  unit(31, W[1], W[0], true, true);
 
   // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[m = wm*64 + i*16 + lane%16][n = wn*128 + j*16 + (lane/16)*4 + e]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // no DMA in flight; every wave done with the W1 stages (reused below)
-  const int nb = wn * 128 + (lane >> 4) * 4;
+  // lane holds C[m = i*16 + lane%16][n = 64w + j*16 + (lane/16)*4 + e]
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const f32x4 b = *(const f32x4*)(b1 + nb + j * 16);
+  for (int j = 0; j < 4; ++j)  // MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(acc[j][0]), "+a"(acc[j][1]), "+a"(acc[j][2]), "+a"(acc[j][3]), "+a"(acc[j][4]),
+                   "+a"(acc[j][5]), "+a"(acc[j][6]), "+a"(acc[j][7]), "+a"(acc[j][8]), "+a"(acc[j][9]),
+                   "+a"(acc[j][10]), "+a"(acc[j][11]), "+a"(acc[j][12]), "+a"(acc[j][13]), "+a"(acc[j][14]),
+                   "+a"(acc[j][15]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live, WV is dead)
+  const int nb = w * 64 + (lane >> 4) * 4;
+  f32x4 bb[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] += b;
-  }
-  float* red = (float*)Wt;  // [BM][2 waves along N] (stride 4)
-  float mean[4], rstd[4];
+  for (int j = 0; j < 4; ++j) bb[j] = *(const f32x4*)(EP + nb + j * 16);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float sum = 0.f;
+  for (int i = 0; i < 16; ++i) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sum += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+    for (int j = 0; j < 4; ++j) t += acc[j][i] + bb[j];
+    float sum = t[0] + t[1] + t[2] + t[3];
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
-    if ((lane >> 4) == 0) red[(wm * 64 + i * 16 + (lane & 15)) * 4 + wn] = sum;
+    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 4 + w] = sum;
+  }
+  __syncthreads();
+  float mean[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 pr = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 4);
+    mean[i] = (pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / BN);
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane & 15)) * 4);
-    mean[i] = (pr[0] + pr[1]) * (1.0f / BN);
-  }
-  __syncthreads();
+  for (int i = 0; i < 16; ++i) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = acc[j][i][e] - mean[i];
-        ss += d * d;
-      }
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 d = acc[j][i] + bb[j] - mean[i];
+      t += d * d;
+    }
+    float ss = t[0] + t[1] + t[2] + t[3];
     ss += __shfl_xor(ss, 16, 64);
     ss += __shfl_xor(ss, 32, 64);
-    if ((lane >> 4) == 0) red[(wm * 64 + i * 16 + (lane & 15)) * 4 + wn] = ss;
+    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 4 + w] = ss;
   }
   __syncthreads();
+  f32x4 gg[4], ee[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane & 15)) * 4);
-    rstd[i] = rsqrtf((pr[0] + pr[1]) * (1.0f / (BN - 1)) + 1e-5f);
+  for (int j = 0; j < 4; ++j) {
+    gg[j] = *(const f32x4*)(EP + 256 + nb + j * 16);
+    ee[j] = *(const f32x4*)(EP + 512 + nb + j * 16);
   }
+  // 16-B stores: for column blocks (j, j+1) a lane of row group R (= lane/16) holds channels 4R..4R+3
+  // of both; v_permlane16_swap trades block j+1 of even groups for block j of odd groups, so even
+  // groups own 8 consecutive channels of block j, odd groups of block j+1 (32 stores per lane, not 64)
   bf16* obase = out + (int64_t)s * out_seq_stride;
+  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
+  const int R = lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const f32x4 ga = *(const f32x4*)(g1 + nb + j * 16);
-    const f32x4 be = *(const f32x4*)(be1 + nb + j * 16);
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 pr = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 4);
+    const float rstd = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
+    const int t = t0 + i * 16 + (lane & 15);
+    uint32_t pk[4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = t0 + wm * 64 + i * 16 + (lane & 15);
-      if (t >= r1) continue;
-      f32x4 v = (acc[j][i] - mean[i]) * rstd[i] * ga + be;
-      store4(obase + (int64_t)t * BN + nb + j * 16, fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f),
-             fmaxf(v[3], 0.f));
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = (acc[j][i] + bb[j] - mean[i]) * rstd * gg[j] + ee[j];
+      pk[j][0] = relu_bf16x2(v[0], v[1]);
+      pk[j][1] = relu_bf16x2(v[2], v[3]);
+    }
+#pragma unroll
+    for (int jp = 0; jp < 4; jp += 2) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(pk[jp][d], pk[jp + 1][d], false, false);
+        pk[jp][d] = sw[0];
+        pk[jp + 1][d] = sw[1];
+      }
+      const int col = w * 64 + (jp + (R & 1)) * 16 + (R >> 1) * 8;
+      const u32x4 o = {pk[jp][0], pk[jp][1], pk[jp + 1][0], pk[jp + 1][1]};
+      buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
     }
   }
+  if constexpr (STAMPS) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+    if (samp >= 0 && tid == 0)
+      for (int k = 0; k < 24 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
+  }
 }
+
 
 }  // namespace
 
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
-                         const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
-                         bf16* out, int64_t out_seq_stride, hipStream_t st, int r0, int r1) {
+                         const float* beta0, const bf16* W1, const bf16* W1s, const float* b1, const float* g1,
+                         const float* be1, bf16* out, int64_t out_seq_stride, hipStream_t st, int r0, int r1,
+                         int grid_cap) {
+  (void)W1;
+  (void)grid_cap;
   if (r1 < 0) r1 = L1;
   if (S <= 0 || L1 <= 0 || r0 < 0 || r1 > L1 || r0 >= r1) return hipErrorInvalidValue;
-  dim3 grid((r1 - r0 + BM - 1) / BM, S);
   static const bool stamps = getenv("VAP_CONV01_STAMPS") != nullptr;
-  static const int ver = getenv("VAP_CONV01_V1") ? 1 : (getenv("VAP_CONV01_V3") ? 3 : 2);
-  if (ver == 1)
-    hipLaunchKernelGGL(conv01_kernel, grid, dim3(512), 0, st, wav, N, L0, L1, (const chunk16*)c0w, c0stat, beta0, W1,
-                       b1, g1, be1, out, out_seq_stride, r0, r1);
-  else if (ver == 2 && !stamps)
-    hipLaunchKernelGGL(conv01b_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1,
-                       b1, g1, be1, out, out_seq_stride, r0, r1);
-  else if (ver == 2)
-    hipLaunchKernelGGL(conv01b_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1,
-                       b1, g1, be1, out, out_seq_stride, r0, r1);
+  static const bool v2 = getenv("VAP_CONV01_V2") != nullptr;  // the whole-phase-image kernel (previous default)
+  if (v2) {
+    dim3 grid((r1 - r0 + BM - 1) / BM, S);
+    if (stamps)
+      hipLaunchKernelGGL(conv01b_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
+                         b1, g1, be1, out, out_seq_stride, r0, r1);
+    else
+      hipLaunchKernelGGL(conv01b_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
+                         W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
+    return hipGetLastError();
+  }
+  dim3 grid((r1 - r0 + BM2 - 1) / BM2, S);
+  static const int diag = getenv("VAP_CONV01_DIAG") ? atoi(getenv("VAP_CONV01_DIAG")) : 0;
+  if (stamps && diag) {  // timing diagnostics only: the outputs are garbage
+#define VAP_DIAG_CASE(D)                                                                                          \
+  case D:                                                                                                         \
+    hipLaunchKernelGGL((conv01i_kernel<true, D>), grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, \
+                       beta0, W1s, b1, g1, be1, out, out_seq_stride, r0, r1);                                     \
+    break;
+    switch (diag) {
+      VAP_DIAG_CASE(2) VAP_DIAG_CASE(4) VAP_DIAG_CASE(6) VAP_DIAG_CASE(8) VAP_DIAG_CASE(20) VAP_DIAG_CASE(36)
+      VAP_DIAG_CASE(68)
+      default: break;
+    }
+#undef VAP_DIAG_CASE
+    return hipGetLastError();
+  }
+  if (stamps)
+    hipLaunchKernelGGL(conv01i_kernel<true>, grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
+                       W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
   else
-    hipLaunchKernelGGL(conv01c_kernel, grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1, b1,
-                       g1, be1, out, out_seq_stride, r0, r1);
+    hipLaunchKernelGGL(conv01i_kernel<false>, grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
+                       W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
   return hipGetLastError();
 }
 
 // diagnostics: copy the conv01 v2 phase stamps (8 sampled workgroups x 24) to host memory
 hipError_t read_conv01_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_conv01_stamps), sizeof(g_conv01_stamps), 0, hipMemcpyDeviceToHost);
+}
+
+// W [N][K] bf16 -> k-step-major [K/32][N][32]: each 32-deep k-step of all N rows is one contiguous
+// block, so a conv01 W1 stage (256 rows x 64 B) is 16 KiB of consecutive lines spread over every L2
+// channel (row-major rows 4 KiB apart hit the same channel)
+__global__ void pack_kstep_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int N, int K) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // output chunk of 8
+  if (i >= (int64_t)N * K / 8) return;
+  const int c = (int)(i & 3), n = (int)((i >> 2) % N), kk = (int)((i >> 2) / N);
+  *(chunk16*)(out + i * 8) = *(const chunk16*)(in + (int64_t)n * K + kk * 32 + c * 8);
+}
+hipError_t launch_pack_kstep(const bf16* in, bf16* out, int N, int K, hipStream_t st) {
+  if (K % 32 || N <= 0) return hipErrorInvalidValue;
+  const int64_t chunks = (int64_t)N * K / 8;
+  hipLaunchKernelGGL(pack_kstep_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, st, in, out, N, K);
+  return hipGetLastError();
 }

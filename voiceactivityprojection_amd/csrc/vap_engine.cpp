@@ -398,6 +398,11 @@ int pack_all(vap_handle* h, hipStream_t st) {
     if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv");
     HIPCHK(launch_pack_conv<T>(h->P(g + ".conv" + std::to_string(i) + ".weight"), w, D, D, kws[i], st));
   }
+  if constexpr (sizeof(T) == 2) {  // conv1 in the k-step-major layout of conv01's W1 stages
+    T* w = alloc("conv1_ks", (int64_t)D * D * kws[1]);
+    if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv1");
+    HIPCHK(launch_pack_kstep((const bf16*)h->W<T>("conv1"), (bf16*)w, D, D * kws[1], st));
+  }
   for (int l = 0; l < h->dims.lstm_layers; ++l) {
     const std::string p = "encoder.encoder.gAR.baseNet.", s = "_l" + std::to_string(l);
     T* wih = alloc("wih" + s, 4 * D * D);
@@ -651,7 +656,7 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   if constexpr (sizeof(T) == 2) {  // fused conv0 -> CN0 -> ReLU -> conv1 -> CN1 -> ReLU (k_conv01.hip)
     Timed tm(h, VAP_K_CONV1, st);
     HIPCHK(launch_conv01(wav + (int64_t)r.s0() * N, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"),
-                         h->fpacked.at("conv0_stat"), h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"),
+                         h->fpacked.at("conv0_stat"), h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), (const bf16*)h->W<T>("conv1_ks"),
                          h->P(g + ".conv1.bias"), h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"),
                          (bf16*)(Xs[0] + D), p.s1, st));
     first = 1;
@@ -964,6 +969,17 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
   return VAP_OK;
 }
 
+// compute units of the current device (persistent kernels size their grid to the CUs they may use)
+static int device_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 // bf16 CPC rows of conv4 range [a4, b4) of every sequence, with the conv1..conv3 rows they need
 // (k4 s2 p1 layers: rows [a, b) need input rows [2a-1, 2b+1) clipped to the layer; conv1 rows come
 // from the fused conv0->conv1 kernel straight from the waveform), then their LSTM gate projections.
@@ -985,9 +1001,9 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   {
     Timed tm(h, VAP_K_CONV1, st);
     HIPCHK(launch_conv01(wav, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"), h->fpacked.at("conv0_stat"),
-                         h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), h->P(g + ".conv1.bias"),
+                         h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), (const bf16*)h->W<T>("conv1_ks"), h->P(g + ".conv1.bias"),
                          h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"), (bf16*)(Xs[0] + D), p.s1, st,
-                         (int)a[0], (int)b[0]));
+                         (int)a[0], (int)b[0], device_cus() - (p.S + 15) / 16));  // the recurrence holds a CU per 16 sequences
   }
   for (int i = 1; i < 4; ++i) {  // conv2..4 (encoder_components.py:100-103)
     const std::string cs = std::to_string(i + 1);

@@ -112,8 +112,11 @@ hipError_t launch_vad_post(const float* vad_probs, int B, int Tn, float cutoff, 
 // bf16 perf mode: fused conv0 -> CN0 -> ReLU -> conv1 -> CN1 -> ReLU (k_conv01.hip).
 // c0w: [256][32] bf16 split-bf16 conv0 operand; c0stat: centred Gram statistics (112 floats).
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
-                         const float* beta0, const bf16* W1, const float* b1, const float* g1, const float* be1,
-                         bf16* out, int64_t out_seq_stride, hipStream_t st, int r0 = 0, int r1 = -1);
+                         const float* beta0, const bf16* W1, const bf16* W1s, const float* b1, const float* g1,
+                         const float* be1, bf16* out, int64_t out_seq_stride, hipStream_t st, int r0 = 0, int r1 = -1,
+                         int grid_cap = 0);
+// W [N][K] bf16 -> k-step-major [K/32][N][32] (conv01's W1 stages as contiguous 16 KiB blocks)
+hipError_t launch_pack_kstep(const bf16* in, bf16* out, int N, int K, hipStream_t st);
 hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CONV01_STAMPS=1)
 hipError_t read_rowpanel_stamps(unsigned long long* out);  // diagnostics (VAP_RP_STAMPS=1)
 hipError_t read_ffn_stamps(unsigned long long* out);  // diagnostics (VAP_FFN_STAMPS=1)
