@@ -7,6 +7,7 @@
  *   vap_create / vap_set_param / vap_finalize   <- VapGPT(conf) + load_state_dict(sd, strict=True)
  *                                                  (vap/model.py:125-163, run.py:199-201)
  *   vap_forward                                 <- VapGPT.forward(waveform)   (vap/model.py:249-268)
+ *   vap_forward_attention                       <- VapGPT.forward(waveform, attention=True)
  *   vap_probs + vap_labels_loss                 <- VapGPT.probs(waveform)     (vap/model.py:180-225)
  *   vap_labels_loss                             <- ObjectiveVAP.get_labels + loss_vap (vap/objective.py:209-243)
  *   vap_frame_lengths                           <- the conv length chain (vap/encoder_components.py:83-92,454-460)
@@ -79,6 +80,17 @@ int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t
 /* waveform [B][2][N] -> logits [B][T][256], vad_logits [B][T][2]. */
 int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
                 float* vad_logits, void* workspace, size_t workspace_bytes, void* stream);
+
+/* VapGPT.forward(waveform, attention=True) (vap/model.py:249-268; GPT / GPTStereo attention outputs,
+ * vap/modules.py:349-356, 400-407): logits / vad_logits as vap_forward plus the softmax attention
+ * weights of every layer, fp32, zeros above the diagonal (causal):
+ *   self_attn       [B][2][channel_layers][H][T][T]  ar_channel self attention, speaker 0 / 1
+ *   cross_attn      [B][2][cross_layers][H][T][T]    ar cross attention (x1 <- x2, x2 <- x1)
+ *   cross_self_attn [B][2][cross_layers][H][T][T]    ar self attention
+ * Any of the three may be NULL.  Runs the layer-by-layer schedule (no time chunks). */
+int vap_forward_attention(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
+                          float* vad_logits, float* self_attn, float* cross_attn, float* cross_self_attn,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* Rolling-window stream (SURVEY config C5; replaces the reference's per-hop model.probs(x) on a
  * rolled window, sds/run_sds.py:206-241 TurnTakingSDS.add_audio_bytes_to_tensor / run, and the

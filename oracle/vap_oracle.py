@@ -156,9 +156,10 @@ def alibi_bias(T: int, m: Tensor, Tk: Optional[int] = None) -> Tensor:
     return rel.unsqueeze(-2) + mask
 
 
-def mha(Q: Tensor, K: Tensor, V: Tensor, sd: SD, prefix: str, num_heads: int) -> Tensor:
+def mha(Q: Tensor, K: Tensor, V: Tensor, sd: SD, prefix: str, num_heads: int, maps: Optional[list] = None) -> Tensor:
     """MultiHeadAttention.forward (modules.py:82-110) with the AliBi mask (modules.py:189-202).
-    Linear projections without bias (:38-40,51); scale = 1/sqrt(dim) (:52, Q5)."""
+    Linear projections without bias (:38-40,51); scale = 1/sqrt(dim) (:52, Q5).  ``maps`` collects
+    the softmax weights (B, H, T, T) the reference returns as ``att`` (:110)."""
     B, T, D = Q.shape
     h = num_heads
 
@@ -171,6 +172,8 @@ def mha(Q: Tensor, K: Tensor, V: Tensor, sd: SD, prefix: str, num_heads: int) ->
     att = torch.einsum("bhid,bhjd->bhij", q, k) * (1.0 / math.sqrt(D))
     att = att + alibi_bias(T, sd[f"{prefix}.m"])
     att = F.softmax(att, dim=-1)
+    if maps is not None:
+        maps.append(att)
     y = (att @ v).transpose(1, 2).reshape(B, T, D)
     return y @ sd[f"{prefix}.proj.weight"].T
 
@@ -179,15 +182,16 @@ def layer_norm(x: Tensor, sd: SD, prefix: str) -> Tensor:
     return F.layer_norm(x, (x.shape[-1],), sd[f"{prefix}.weight"], sd[f"{prefix}.bias"])
 
 
-def transformer_layer(x: Tensor, sd: SD, prefix: str, num_heads: int, src: Optional[Tensor] = None) -> Tensor:
+def transformer_layer(x: Tensor, sd: SD, prefix: str, num_heads: int, src: Optional[Tensor] = None,
+                      smaps: Optional[list] = None, cmaps: Optional[list] = None) -> Tensor:
     """TransformerLayer.forward (modules.py:246-275), eval mode (dropout = identity).
     Pre-LN self-attn + residual; cross-attn Q = LN_src(x), K = V = raw src (:265-272); FFN
     (ffn_block :9-21: Linear -> GELU -> Linear, no bias) + residual."""
     z = layer_norm(x, sd, f"{prefix}.ln_self_attn")
-    x = x + mha(z, z, z, sd, f"{prefix}.mha", num_heads)
+    x = x + mha(z, z, z, sd, f"{prefix}.mha", num_heads, smaps)
     if src is not None:
         z = layer_norm(x, sd, f"{prefix}.ln_src_attn")
-        x = x + mha(z, src, src, sd, f"{prefix}.mha_cross", num_heads)
+        x = x + mha(z, src, src, sd, f"{prefix}.mha_cross", num_heads, cmaps)
     z = layer_norm(x, sd, f"{prefix}.ln_ffnetwork")
     z = F.gelu(z @ sd[f"{prefix}.ffnetwork.0.weight"].T) @ sd[f"{prefix}.ffnetwork.3.weight"].T
     return x + z
@@ -200,10 +204,10 @@ def count_layers(sd: SD, prefix: str) -> int:
     return n
 
 
-def gpt(x: Tensor, sd: SD, num_heads: int) -> Tensor:
+def gpt(x: Tensor, sd: SD, num_heads: int, smaps: Optional[list] = None) -> Tensor:
     """GPT.forward (modules.py:342-358) for ``ar_channel``."""
     for l in range(count_layers(sd, "ar_channel")):
-        x = transformer_layer(x, sd, f"ar_channel.layers.{l}", num_heads)
+        x = transformer_layer(x, sd, f"ar_channel.layers.{l}", num_heads, smaps=smaps)
     return x
 
 
@@ -214,13 +218,15 @@ def combinator(x1: Tensor, x2: Tensor, sd: SD) -> Tensor:
     return ha + hb
 
 
-def gpt_stereo(x1: Tensor, x2: Tensor, sd: SD, num_heads: int):
+def gpt_stereo(x1: Tensor, x2: Tensor, sd: SD, num_heads: int, maps: Optional[dict] = None):
     """GPTStereo.forward (modules.py:380-408) + TransformerStereoLayer (:279-289): both towers use
-    the PRE-layer x1/x2 as each other's src."""
+    the PRE-layer x1/x2 as each other's src.  ``maps`` collects the per-layer weights of each tower
+    under "sa" / "ca" (self / cross) as lists [tower a, tower b]."""
+    m = maps if maps is not None else {"sa": [[], []], "ca": [[], []]}
     for l in range(count_layers(sd, "ar")):
         p = f"ar.layers.{l}"
-        z1 = transformer_layer(x1, sd, p, num_heads, src=x2)
-        z2 = transformer_layer(x2, sd, p, num_heads, src=x1)
+        z1 = transformer_layer(x1, sd, p, num_heads, src=x2, smaps=m["sa"][0], cmaps=m["ca"][0])
+        z2 = transformer_layer(x2, sd, p, num_heads, src=x1, smaps=m["sa"][1], cmaps=m["ca"][1])
         x1, x2 = z1, z2
     return combinator(x1, x2, sd), x1, x2
 
@@ -228,22 +234,34 @@ def gpt_stereo(x1: Tensor, x2: Tensor, sd: SD, num_heads: int):
 # --------------------------------------------------------------------------------------------
 # A15-A20 model forward / probs / objective
 # --------------------------------------------------------------------------------------------
-def forward(waveform: Tensor, sd: SD, num_heads: int = 4, taps: Optional[dict] = None) -> Dict[str, Tensor]:
-    """VapGPT.forward (model.py:249-268). waveform (B, 2, N) -> logits (B,T,256), vad (B,T,2)."""
+def forward(waveform: Tensor, sd: SD, num_heads: int = 4, taps: Optional[dict] = None,
+            attention: bool = False) -> Dict[str, Tensor]:
+    """VapGPT.forward (model.py:249-268). waveform (B, 2, N) -> logits (B,T,256), vad (B,T,2); with
+    ``attention`` also self_attn (B,2,Lc,H,T,T), cross_attn / cross_self_attn (B,2,Lx,H,T,T)
+    (model.py:264-267, modules.py:349-356 / 400-407)."""
     assert waveform.shape[1] == 2, f"audio VAP ENCODER: {waveform.shape} != (B, 2, n_samples)"
     x1 = encoder(waveform[:, :1], sd, taps)  # model.py:173-174
     x2 = encoder(waveform[:, 1:], sd, None)
     if taps is not None:
         taps["enc1"], taps["enc2"] = x1, x2
-    o1 = gpt(x1, sd, num_heads)
-    o2 = gpt(x2, sd, num_heads)
+    s1, s2 = [], []
+    o1 = gpt(x1, sd, num_heads, s1)
+    o2 = gpt(x2, sd, num_heads, s2)
     if taps is not None:
         taps["ar_channel1"], taps["ar_channel2"] = o1, o2
-    x, y1, y2 = gpt_stereo(o1, o2, sd, num_heads)
+    maps = {"sa": [[], []], "ca": [[], []]}
+    x, y1, y2 = gpt_stereo(o1, o2, sd, num_heads, maps)
     w, b = sd["va_classifier.weight"], sd["va_classifier.bias"]
     vad = torch.cat((y1 @ w.T + b, y2 @ w.T + b), dim=-1)
     logits = x @ sd["vap_head.weight"].T + sd["vap_head.bias"]
-    return {"logits": logits, "vad": vad}
+    ret = {"logits": logits, "vad": vad}
+    if attention:
+        def stk(a, b):  # per tower: layers stacked on dim 1, then towers on dim 1
+            return torch.stack([torch.stack(a, dim=1), torch.stack(b, dim=1)], dim=1)
+        ret["self_attn"] = stk(s1, s2)
+        ret["cross_attn"] = stk(*maps["ca"])
+        ret["cross_self_attn"] = stk(*maps["sa"])
+    return ret
 
 
 def aggregate_matrix(n_bins: int, from_bin: int, to_bin: int) -> Tensor:

@@ -71,7 +71,7 @@ def test_model_properties():
     assert m.horizon_time == pytest.approx(2.0)
     assert m.sample_rate == 16000 and m.frame_hz == 50
     assert m.objective.n_classes == 256 and m.objective.horizon == 100
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="no CPU fallback"):  # attention maps run on the engine too
         m(torch.zeros(1, 2, 40960), attention=True)
 
 

@@ -237,3 +237,39 @@ def test_bench_shape_bf16(m16, m32):
             assert err <= BF16_TOL[k], (k, i, err)
     for k in ("probs", "p_now", "p_future", "vad", "H", "loss"):
         assert torch.isfinite(full[k]).all(), k
+
+
+ATTN_KEYS = ("self_attn", "cross_attn", "cross_self_attn")
+
+
+def test_attention_maps_fp32_vs_reference(m32, golden):
+    """forward(attention=True) (model.py:249-268): every layer's softmax weights against the
+    reference's own maps (tests/golden/attention_maps.npz), fp32 mode, 1e-4 absolute."""
+    g = golden("attention_maps")
+    w = torch.from_numpy(g["waveform"]).cuda()
+    out = m32(w, attention=True)
+    for k in ("logits",) + ATTN_KEYS:
+        got = out[k].cpu().numpy()
+        assert got.shape == g[k].shape, (k, got.shape, g[k].shape)
+        err = float(np.abs(got - g[k]).max())
+        assert err < 1e-4, f"{k}: {err}"
+    np.testing.assert_allclose(out["vad"].cpu().numpy(), g["vad_logits"], atol=1e-4)
+    # rows are distributions over the causal past; the plain forward gives the same logits
+    sa = out["self_attn"]
+    assert torch.allclose(sa.sum(-1), torch.ones_like(sa.sum(-1)), atol=1e-5)
+    assert float(torch.triu(sa, diagonal=1).abs().max()) == 0.0
+    plain = m32(w)
+    assert torch.equal(plain["logits"], out["logits"])
+
+
+def test_attention_maps_bf16_vs_oracle(m16):
+    """bf16 mode maps on a 2-clip batch against the oracle (fp32) on the same input."""
+    wav = np.stack([synthetic_waveform(i, 16000) for i in (30, 31)])
+    out = m16(torch.from_numpy(wav).cuda(), attention=True)
+    ref = O.forward(torch.from_numpy(wav), O.state_dict_to_torch(synthetic_state_dict(seed=0)), attention=True)
+    for k in ATTN_KEYS:
+        got = out[k].cpu().numpy()
+        exp = ref[k].numpy()
+        assert got.shape == exp.shape, (k, got.shape, exp.shape)
+        err = float(np.abs(got - exp).max())
+        assert err < 3e-2, f"{k}: {err}"

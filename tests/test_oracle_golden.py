@@ -104,3 +104,16 @@ def test_labels_bit_exact(golden):
     got = O.get_labels_np(soft, [10, 20, 30, 40])
     np.testing.assert_array_equal(got[safe], g["soft_labels"][safe])
     assert safe.mean() > 0.95
+
+
+def test_oracle_attention_maps_vs_reference(golden):
+    """attention=True maps of the oracle against the reference's own (tools/gen_golden.py attention)."""
+    g = golden("attention_maps")
+    sd = _sd()
+    out = O.forward(torch.from_numpy(g["waveform"]), sd, attention=True)
+    for k in ("logits", "vad_logits", "self_attn", "cross_attn", "cross_self_attn"):
+        ref = g[k]
+        got = out["vad" if k == "vad_logits" else k].numpy()
+        assert got.shape == ref.shape, (k, got.shape, ref.shape)
+        err = float(np.abs(got - ref).max())
+        assert err < 1e-5, f"{k}: {err}"

@@ -11,6 +11,7 @@ Weights are the deterministic synthetic ones from ``voiceactivityprojection_amd.
 with ``strict=True``.  Outputs land in ``tests/golden/*.npz`` (inputs + expected outputs only).
 
 Usage:  python tools/gen_golden.py            (takes ~1 min on 8 CPU threads)
+        python tools/gen_golden.py attention  (only the attention-map fixture)
 """
 from __future__ import annotations
 
@@ -187,5 +188,24 @@ def main():
     print("wrote", sorted(os.listdir(OUT)))
 
 
+def gen_attention():
+    """(g) VapGPT.forward(attention=True) maps (model.py:264-267) of a 0.8 s clip (T = 40): every
+    layer's self / cross / cross-self softmax weights, (1, 2, L, H, T, T)."""
+    torch.set_num_threads(8)
+    model = build_model(1)
+    n = 12800
+    wav = synthetic_waveform(21, n)[None]
+    with torch.no_grad():
+        out = model(torch.from_numpy(wav), attention=True)
+    np.savez_compressed(os.path.join(OUT, "attention_maps.npz"), waveform=wav, logits=out["logits"].numpy(),
+                        vad_logits=out["vad"].numpy(), self_attn=out["self_attn"].numpy(),
+                        cross_attn=out["cross_attn"].numpy(), cross_self_attn=out["cross_self_attn"].numpy())
+    print("wrote attention_maps.npz", {k: tuple(v.shape) for k, v in out.items()})
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "attention":
+        gen_attention()
+    else:
+        main()
+        gen_attention()

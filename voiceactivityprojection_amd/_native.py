@@ -43,6 +43,7 @@ _SIGS = {
     "vap_frame_lengths": (ctypes.c_int, [_I64, ctypes.POINTER(_I64)]),
     "vap_workspace_size": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.POINTER(ctypes.c_size_t)]),
     "vap_forward": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, _P, ctypes.c_size_t, _P]),
+    "vap_forward_attention": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "vap_encode": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, ctypes.c_size_t, _P]),
     "vap_stream_create": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P]),
     "vap_stream_push": (ctypes.c_int, [_P, _P, _P, _P, _P]),

@@ -538,3 +538,58 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
 
 template hipError_t launch_attention<float>(const AttnArgs&, hipStream_t);
 template hipError_t launch_attention<bf16>(const AttnArgs&, hipStream_t);
+
+// ------------------------------------------------------------------------------------------
+// Attention weights (VapGPT.forward(attention=True), vap/model.py:264-267; the `att` the reference
+// MultiHeadAttention returns, modules.py:96-110): softmax(q k^T * scale + m_h * j, causal) rows,
+// materialised as P[s][h][i][j] (fp32, zeros above the diagonal).  A diagnostic path, not the hot
+// one: one wave per query row, fp32 dot products from the layer's Q / K (fp32 or bf16 storage).
+// The AliBi term uses m_h * (j - i), equal after the row softmax to the reference's m_h * j.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void attn_probs_kernel(AttnArgs a, float* __restrict__ out, int64_t out_seq,
+                                                         int64_t out_head) {
+  __shared__ float qs[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 4 + w, h = blockIdx.y, s = blockIdx.z;
+  if (i >= a.T) return;  // wave-uniform; no block-wide sync below
+  const T* Q = (const T*)a.Q + (int64_t)s * a.q_seq + (int64_t)i * a.q_ld + h * 64;
+  const int skv = a.kv_swap ? (s ^ 1) : s;
+  const T* K = (const T*)a.K + (int64_t)skv * a.k_seq + h * 64;
+  qs[w][lane] = to_f32(Q[lane]) * a.scale;
+  __builtin_amdgcn_wave_barrier();
+  const float m = a.slopes[h];
+  float* o = out + (int64_t)s * out_seq + (int64_t)h * out_head + (int64_t)i * a.T;
+  // pass 1: scores of keys j = lane + 64 t (j <= i) -> row max
+  float mx = -INFINITY;
+  for (int j = lane; j <= i; j += 64) {
+    const T* k = K + (int64_t)j * a.k_ld;
+    float d = 0.f;
+#pragma unroll 16
+    for (int c = 0; c < 64; ++c) d = fmaf(qs[w][c], to_f32(k[c]), d);
+    const float v = d + m * (float)(j - i);
+    o[j] = v;  // scratch: the raw score, rewritten below
+    mx = fmaxf(mx, v);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j <= i; j += 64) {
+    const float e = __expf(o[j] - mx);
+    o[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  const float inv = 1.0f / sum;
+  for (int j = lane; j < a.T; j += 64) o[j] = j <= i ? o[j] * inv : 0.f;
+}
+}  // namespace
+
+template <typename T>
+hipError_t launch_attn_probs(const AttnArgs& a, float* out, int64_t out_seq, int64_t out_head, hipStream_t st) {
+  if (a.T <= 0 || a.S <= 0 || a.H <= 0 || !out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((attn_probs_kernel<T>), dim3((a.T + 3) / 4, a.H, a.S), dim3(256), 0, st, a, out, out_seq, out_head);
+  return hipGetLastError();
+}
+template hipError_t launch_attn_probs<float>(const AttnArgs&, float*, int64_t, int64_t, hipStream_t);
+template hipError_t launch_attn_probs<bf16>(const AttnArgs&, float*, int64_t, int64_t, hipStream_t);

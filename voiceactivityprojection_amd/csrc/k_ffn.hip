@@ -27,8 +27,8 @@ namespace {
 constexpr int BM = 64, D = 256, DF = 768;
 constexpr int PROWB = D * 2;                  // LN panel row: 512 B (32 chunks)
 constexpr int HROWB = DF * 2;                 // hidden row: 1536 B (96 chunks)
-constexpr int OFF_H = BM * PROWB;             // 32 KiB
-constexpr int LDS_BYTES = OFF_H + BM * HROWB;  // + 96 KiB = 128 KiB
+// MT row tiles of 16 per workgroup (BM = 16 MT rows): LN panel 512 B + hidden 1536 B per row
+template <int MT> constexpr int ffn_lds() { return MT * 16 * (PROWB + HROWB); }  // MT 4: 128 KiB, 5: 160 KiB
 constexpr int NF1 = 6, NF2 = 2;               // weight fragments per wave: up / down
 constexpr int KS1 = D / 32, KS2 = DF / 32;    // k-steps: 8 / 24
 constexpr int NPF1 = 2, NPF2 = 4;             // weight prefetch depth (k-steps)
@@ -44,13 +44,14 @@ VAP_DEV int xswz(int row, int c) { return c ^ (row & 15); }
 __device__ unsigned long long g_ffn_stamps[8][24];
 __device__ unsigned long long g_ffn_wall[1024][2];  // every workgroup < 1024: realtime start / end
 
-template <bool ST>
+template <bool ST, int MT>
 __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  constexpr int BMt = MT * 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[ffn_lds<MT>()];
   unsigned char* P = smem;
-  unsigned char* Hh = smem + OFF_H;
+  unsigned char* Hh = smem + BMt * PROWB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int m0 = blockIdx.x * BM;
+  const int m0 = blockIdx.x * BMt;
   const bf16* __restrict__ W1 = (const bf16*)g.W1;
   const bf16* __restrict__ W2 = (const bf16*)g.W2;
   const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && tid == 0) ? (int)(blockIdx.x >> 6) : -1;
@@ -75,12 +76,14 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   // wave w: rows w*8 .. w*8+7 as 2 sets of 4; a 16-lane group reads 256 contiguous bytes of its row
   // per load.  Loads are unconditional (clamped row + select): a load under a branch gets its own
   // s_waitcnt and serialises the panel.
+  // 4-row sets s = w, w + 8, ... (BM / 4 sets over the 8 waves)
+  constexpr int NSET = (BMt / 4 + 7) / 8;
   {
     const int r4 = lane >> 4, cc = lane & 15;
-    f32x4 v[2][4];
+    f32x4 v[NSET][4];
 #pragma unroll
-    for (int set = 0; set < 2; ++set) {
-      const int m = m0 + w * 8 + set * 4 + r4;
+    for (int set = 0; set < NSET; ++set) {
+      const int m = m0 + (w + set * 8) * 4 + r4;
       const float* src = g.x + xoff(m < g.M ? m : g.M - 1) + cc * 4;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) v[set][jj] = *(const f32x4*)(src + jj * 64);
@@ -92,7 +95,8 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
       be[jj] = *(const f32x4*)(g.beta + jj * 64 + cc * 4);
     }
 #pragma unroll
-    for (int set = 0; set < 2; ++set) {
+    for (int set = 0; set < NSET; ++set) {
+      if (w + set * 8 >= BMt / 4) break;
       float sum = 0.f;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) sum += v[set][jj][0] + v[set][jj][1] + v[set][jj][2] + v[set][jj][3];
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o, 64);
       const float rstd = rsqrtf(ss * (1.0f / D) + g.eps);
-      const int row = w * 8 + set * 4 + r4;
+      const int row = (w + set * 8) * 4 + r4;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {  // rows >= M hold LN(row M-1): computed, never stored
         const f32x4 y = v[set][jj] * rstd * ga[jj] + be[jj];
@@ -136,17 +140,17 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   __syncthreads();  // LN panel complete
   stamp(2);
 
-  f32x4 acc1[NF1][4];
+  f32x4 acc1[NF1][MT];
 #pragma unroll
   for (int i = 0; i < NF1; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < MT; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS1; ++ks) {
     stamp(3 + ks);
-    chunk16 af[4];
+    chunk16 af[MT];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < MT; ++j) {
       const int row = j * 16 + (lane & 15);
       af[j] = *(const chunk16*)(P + row * PROWB + xswz(row, ks * 4 + (lane >> 4)) * 16);
     }
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
 #pragma unroll
     for (int i = 0; i < NF1; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc1[i][j] = mfma_chunk<bf16>(wf[i], af[j], acc1[i][j]);
+      for (int j = 0; j < MT; ++j) acc1[i][j] = mfma_chunk<bf16>(wf[i], af[j], acc1[i][j]);
     // unconditional refill (the tail reloads the last step): conditional loads make the compiler's
     // vmcnt bookkeeping drain the whole prefetch
     w1load(ks + NPF1 < KS1 ? ks + NPF1 : KS1 - 1, wf);
@@ -174,18 +178,18 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   // this lane's 4 rows (j*16 + lane%16) as byte offsets from the panel's first row of x; rows >= M
   // are out of range for the buffer resource: their residual reads return 0, their stores drop
   const int64_t xbase = xoff(m0);
-  uint32_t xrow[4];
+  uint32_t xrow[MT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < MT; ++j) {
     const int m = m0 + j * 16 + (lane & 15);
     xrow[j] = m < g.M ? (uint32_t)((xoff(m) - xbase) * 4) : 0x80000000u;
   }
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
-  f32x4 res[NF2][4];
+  f32x4 res[NF2][MT];
 #pragma unroll
   for (int i = 0; i < NF2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < MT; ++j)
       res[i][j] = __builtin_bit_cast(f32x4, buf_load16(rx, xrow[j] + (uint32_t)(w * 32 + i * 16 + (lane >> 4) * 4) * 4u, 0));
 
   // GELU -> bf16 hidden image: lane holds hidden columns n .. n+3 of row j*16 + lane%16
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   for (int i = 0; i < NF1; ++i) {
     const int n = (w * NF1 + i) * 16 + (lane >> 4) * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < MT; ++j) {
       const int row = j * 16 + (lane & 15);
       const f32x4 a = acc1[i][j];
       const f32x2 lo = gelu_fast2((f32x2){a[0], a[1]}), hi = gelu_fast2((f32x2){a[2], a[3]});
@@ -206,19 +210,19 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
   stamp(13);
 
   // ------------------------------------------------------------ FFN-down: 24 k-steps, N 256
-  f32x4 acc2[NF2][4];
+  f32x4 acc2[NF2][MT];
 #pragma unroll
   for (int i = 0; i < NF2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < MT; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto hread = [&](int ks, chunk16* af) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < MT; ++j) {
       const int row = j * 16 + (lane & 15);
       af[j] = *(const chunk16*)(Hh + row * HROWB + xswz(row, ks * 4 + (lane >> 4)) * 16);
     }
   };
-  chunk16 ha[2][4];
+  chunk16 ha[2][MT];
   hread(0, ha[0]);
 #pragma unroll
   for (int ks = 0; ks < KS2; ++ks) {
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
 #pragma unroll
     for (int i = 0; i < NF2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc2[i][j] = mfma_chunk<bf16>(wf[i], ha[ks & 1][j], acc2[i][j]);
+      for (int j = 0; j < MT; ++j) acc2[i][j] = mfma_chunk<bf16>(wf[i], ha[ks & 1][j], acc2[i][j]);
     w2load(ks + NPF2 < KS2 ? ks + NPF2 : KS2 - 1, wf);
   }
 
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
 #pragma unroll
   for (int i = 0; i < NF2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < MT; ++j) {
       const f32x4 v = res[i][j] + acc2[i][j];
       buf_store16_wt(rx, xrow[j] + (uint32_t)(w * 32 + i * 16 + (lane >> 4) * 4) * 4u, __builtin_bit_cast(u32x4, v));
     }
@@ -253,14 +257,22 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(FfnArgs g) {
 
 hipError_t launch_ffn(const FfnArgs& g, hipStream_t st) {
   if (g.M <= 0 || g.rows_per_seq < 0) return hipErrorInvalidValue;
+  // 64-row panels; VAP_FFN_MT=5: 80-row panels (the whole 160 KiB of LDS), measured equal on the
+  // bench (400 workgroups instead of 500 over the 248 CUs the concurrent LSTM leaves)
+  static const int mt = getenv("VAP_FFN_MT") ? atoi(getenv("VAP_FFN_MT")) : 4;
+  const int bm = (mt == 4 ? 4 : 5) * 16;
   // a panel's rows must lie within the 2 GiB a buffer offset reaches from its first row
-  const int64_t span = g.rows_per_seq ? (BM / g.rows_per_seq + 2) * g.x_seq + (int64_t)BM * D : (int64_t)BM * D;
+  const int64_t span = g.rows_per_seq ? (bm / g.rows_per_seq + 2) * g.x_seq + (int64_t)bm * D : (int64_t)bm * D;
   if (span * 4 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
   static const bool stamps = getenv("VAP_FFN_STAMPS") != nullptr;
-  if (stamps)
-    hipLaunchKernelGGL(ffn_kernel<true>, dim3((g.M + BM - 1) / BM), dim3(512), 0, st, g);
-  else
-    hipLaunchKernelGGL(ffn_kernel<false>, dim3((g.M + BM - 1) / BM), dim3(512), 0, st, g);
+  const dim3 grid((g.M + bm - 1) / bm);
+  if (mt == 4) {
+    if (stamps) hipLaunchKernelGGL((ffn_kernel<true, 4>), grid, dim3(512), 0, st, g);
+    else hipLaunchKernelGGL((ffn_kernel<false, 4>), grid, dim3(512), 0, st, g);
+  } else {
+    if (stamps) hipLaunchKernelGGL((ffn_kernel<true, 5>), grid, dim3(512), 0, st, g);
+    else hipLaunchKernelGGL((ffn_kernel<false, 5>), grid, dim3(512), 0, st, g);
+  }
   return hipGetLastError();
 }
 

@@ -121,6 +121,10 @@ struct vap_handle {
   const float* P(const std::string& k) const { return params.at(k).dev; }
   template <typename T>
   const T* W(const std::string& k) const { return (const T*)packed.at(k); }
+  // attention=True: attention-weight outputs (channel self / cross / cross-layer self), set only for
+  // the duration of vap_forward_attention
+  float* amap[3] = {nullptr, nullptr, nullptr};
+  bool amap_active() const { return amap[0] || amap[1] || amap[2]; }
 };
 
 namespace {
@@ -484,8 +488,19 @@ struct Range {
 
 // bf16 transformer layer on row-panel kernels: LayerNorm fused into the A-panel load of the
 // Q/K/V, cross-Q and FFN-up projections; residual adds fused into the output projections.
+// attention weights of layer `layer` (attention=True only): which = 0 channel self, 1 cross, 2 cross self
+template <typename T>
+int attn_maps(vap_handle* h, const AttnArgs& a, int which, int layer, Range r, hipStream_t st) {
+  if (!h->amap[which]) return VAP_OK;
+  const int L = which == 0 ? h->dims.channel_layers : h->dims.cross_layers;
+  const int64_t TT = (int64_t)a.T * a.T, per_seq = (int64_t)L * a.H * TT;
+  float* out = h->amap[which] + (int64_t)r.s0() * per_seq + (int64_t)layer * a.H * TT;
+  HIPCHK(launch_attn_probs<T>(a, out, per_seq, TT, st));
+  return VAP_OK;
+}
+
 int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
-                hipStream_t st) {
+                hipStream_t st, int layer) {
   using T = bf16;
   const int T_ = p.T;
   const int S = r.ns();
@@ -518,6 +533,7 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, T_, H,
                0, scale};
     HIPCHK(launch_attention<T>(a, st));
+    if (int rc = attn_maps<T>(h, a, cross ? 2 : 0, layer, r, st)) return rc;
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
@@ -533,6 +549,7 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, T_, H, 1,
                  scale};
       HIPCHK(launch_attention<T>(a, st));
+      if (int rc = attn_maps<T>(h, a, 1, layer, r, st)) return rc;
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
@@ -559,9 +576,9 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
 
 template <typename T>
 int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
-             hipStream_t st) {
+             hipStream_t st, int layer) {
   if constexpr (sizeof(T) == 2) {
-    if (!h->legacy_tr) return tr_layer_rp(h, p, ws, pre, cross, r, st);
+    if (!h->legacy_tr) return tr_layer_rp(h, p, ws, pre, cross, r, st, layer);
   }
   const int T_ = p.T;
   const int S = r.ns();
@@ -600,6 +617,7 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
     AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, T_, H,
                0, scale};
     HIPCHK(launch_attention<T>(a, st));
+    if (int rc = attn_maps<T>(h, a, cross ? 2 : 0, layer, r, st)) return rc;
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
@@ -620,6 +638,7 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
       AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, T_, H, 1,
                  scale};
       HIPCHK(launch_attention<T>(a, st));
+      if (int rc = attn_maps<T>(h, a, 1, layer, r, st)) return rc;
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
@@ -785,9 +804,9 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
   }
   int rc;
   for (int l = 0; l < h->dims.channel_layers; ++l)
-    if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, r, st))) return rc;
+    if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, r, st, l))) return rc;
   for (int l = 0; l < h->dims.cross_layers; ++l)
-    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, r, st))) return rc;
+    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, r, st, l))) return rc;
 
   return heads<T>(h, p, ws, r, logits, vadl, st);
 }
@@ -1082,7 +1101,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   const int NL = h->dims.lstm_layers;
   int m = h->microbatches < 1 ? 1 : h->microbatches;
   if (m > B) m = B;
-  if (NL > 1) m = 1;  // stacked LSTMs: keep the simple serial schedule
+  if (NL > 1 || h->amap_active()) m = 1;  // stacked LSTMs / attention maps: the simple serial schedule
   std::vector<Range> rs;
   for (int i = 0; i < m; ++i) {
     const int c0 = (int)((int64_t)B * i / m), c1 = (int)((int64_t)B * (i + 1) / m);
@@ -1090,7 +1109,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   }
   int rc;
   if constexpr (sizeof(T) == 2) {
-    if (h->use_time_chunks() && !enc_out && p.QKVL) {
+    if (h->use_time_chunks() && !enc_out && p.QKVL && !h->amap_active()) {
       if ((rc = h->ensure_streams())) return rc;
       if (h->wait_value) return run_forward_tc(h, p, wav, N, logits, vadl, ws, st);
     }
@@ -1398,6 +1417,18 @@ int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_sampl
                                  (hipStream_t)stream)
              : run_forward<float>(h, waveform, batch, n_samples, logits, vad_logits, (unsigned char*)workspace,
                                   (hipStream_t)stream);
+}
+
+int vap_forward_attention(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
+                          float* vad_logits, float* self_attn, float* cross_attn, float* cross_self_attn,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  h->amap[0] = self_attn;
+  h->amap[1] = cross_attn;
+  h->amap[2] = cross_self_attn;
+  const int rc = vap_forward(h, waveform, batch, n_samples, logits, vad_logits, workspace, workspace_bytes, stream);
+  h->amap[0] = h->amap[1] = h->amap[2] = nullptr;
+  return rc;
 }
 
 int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t hop_samples, void* stream,

@@ -84,6 +84,9 @@ struct AttnArgs {
 };
 template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);
+// attention weights of one layer (attention=True): out[s * out_seq + h * out_head + i * T + j] fp32
+template <typename T>
+hipError_t launch_attn_probs(const AttnArgs& a, float* out, int64_t out_seq, int64_t out_head, hipStream_t st);
 
 // va_classifier on both towers: vad[b][t][c] = dot(x[2b+c][t], w) + bias (x fp32, clip-major seqs)
 hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const float* bias, float* vad, hipStream_t st);

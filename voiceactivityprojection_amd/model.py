@@ -253,10 +253,11 @@ class VapGPT(nn.Module):
         return out[0], out[1]
 
     def forward(self, waveform: Tensor, attention: bool = False) -> Dict[str, Tensor]:
-        """vap/model.py:249-268 -> {"logits": (B, T, 256), "vad": (B, T, 2)}."""
+        """vap/model.py:249-268 -> {"logits": (B, T, 256), "vad": (B, T, 2)}; with ``attention=True`` also
+        "self_attn" (B, 2, channel_layers, H, T, T), "cross_attn" and "cross_self_attn"
+        (B, 2, cross_layers, H, T, T): the softmax weights of every layer (model.py:264-267)."""
         if attention:
-            raise NotImplementedError("attention maps (attention=True) are not produced by the MI355X engine "
-                                      "(SURVEY.md §8(f) rank 4)")
+            return self._forward_attention(waveform)
         waveform = self._check_input(waveform)
         B, _, n = waveform.shape
         T = N.frame_lengths(n)[-1]
@@ -269,6 +270,28 @@ class VapGPT(nn.Module):
         N.check(N.lib().vap_forward(h, waveform.data_ptr(), B, n, logits.data_ptr(), vad.data_ptr(), ws.data_ptr(),
                                     ws.numel(), N.stream_ptr(waveform.device)), "vap_forward")
         return {"logits": logits, "vad": vad}
+
+    def _forward_attention(self, waveform: Tensor) -> Dict[str, Tensor]:
+        waveform = self._check_input(waveform)
+        B, _, n = waveform.shape
+        T = N.frame_lengths(n)[-1]
+        if T <= 0:
+            raise RuntimeError(f"waveform of {n} samples is too short for one frame")
+        c = self.conf
+        dev = waveform.device
+        h = self._native(dev)
+        ws = self._workspace(h, B, n, dev)
+        logits = torch.empty(B, T, self.objective.n_classes, device=dev, dtype=torch.float32)
+        vad = torch.empty(B, T, 2, device=dev, dtype=torch.float32)
+        sa = torch.empty(B, 2, c.channel_layers, c.num_heads, T, T, device=dev, dtype=torch.float32)
+        ca = torch.empty(B, 2, c.cross_layers, c.num_heads, T, T, device=dev, dtype=torch.float32)
+        csa = torch.empty_like(ca)
+        N.check(N.lib().vap_forward_attention(h, waveform.data_ptr(), B, n, logits.data_ptr(), vad.data_ptr(),
+                                              sa.data_ptr() if sa.numel() else None,
+                                              ca.data_ptr() if ca.numel() else None,
+                                              csa.data_ptr() if csa.numel() else None, ws.data_ptr(), ws.numel(),
+                                              N.stream_ptr(dev)), "vap_forward_attention")
+        return {"logits": logits, "vad": vad, "self_attn": sa, "cross_attn": ca, "cross_self_attn": csa}
 
     @torch.no_grad()
     def probs(self, waveform: Tensor, vad: Optional[Tensor] = None, now_lims: List[int] = [0, 1],
