@@ -8,6 +8,7 @@
  *                                                  (vap/model.py:125-163, run.py:199-201)
  *   vap_forward                                 <- VapGPT.forward(waveform)   (vap/model.py:249-268)
  *   vap_forward_attention                       <- VapGPT.forward(waveform, attention=True)
+ *   vap_forward_mono                            <- VapGPTMono.forward(waveform, va, va_history)  (vap/model.py:271-393)
  *   vap_probs + vap_labels_loss                 <- VapGPT.probs(waveform)     (vap/model.py:180-225)
  *   vap_labels_loss                             <- ObjectiveVAP.get_labels + loss_vap (vap/objective.py:209-243)
  *   vap_frame_lengths                           <- the conv length chain (vap/encoder_components.py:83-92,454-460)
@@ -58,6 +59,8 @@ typedef struct vap_dims {
   int lstm_layers;    /* CPCAR nLevelsGRU (from the state dict) */
   int n_bins;         /* len(VapConfig.bin_times) (must be 4: 256 classes) */
   int precision;      /* VAP_PRECISION_* */
+  int mono;           /* 1: VapGPTMono (vap/model.py:271-393): one speaker + VA conditioning, plain GPT stack */
+  int va_history_bins;/* VapMonoConfig.va_history_bins when va_history (mono only), else 0 */
 } vap_dims;
 
 typedef struct vap_handle vap_handle;
@@ -91,6 +94,16 @@ int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_sampl
 int vap_forward_attention(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits,
                           float* vad_logits, float* self_attn, float* cross_attn, float* cross_self_attn,
                           void* workspace, size_t workspace_bytes, void* stream);
+
+/* VapGPTMono.forward(waveform, va, va_history) (vap/model.py:360-393) on a dims.mono handle:
+ * waveform [B][1][N], va [B][T][2] (voice activity conditioning), va_history [B][T][bins] or NULL
+ * -> logits [B][T][256] (the reference returns `va` itself as "vad").  vap_encode on a mono handle
+ * writes [B][T][256]. */
+int vap_forward_mono(vap_handle* h, const float* waveform, const float* va, const float* va_history, int batch,
+                     int64_t n_samples, float* logits, void* workspace, size_t workspace_bytes, void* stream);
+/* VapGPTMono.encode_va (vap/model.py:352-357): out [rows][256] = LN(va_condition(va [rows][2])
+ * [+ va_cond_history(va_history [rows][bins])]); va_history may be NULL. */
+int vap_encode_va(vap_handle* h, const float* va, const float* va_history, int rows, float* out, void* stream);
 
 /* Rolling-window stream (SURVEY config C5; replaces the reference's per-hop model.probs(x) on a
  * rolled window, sds/run_sds.py:206-241 TurnTakingSDS.add_audio_bytes_to_tensor / run, and the

@@ -360,3 +360,41 @@ def probs(waveform: Tensor, sd: SD, num_heads: int = 4, bin_frames: Optional[Lis
 
 def state_dict_to_torch(sd_np: Dict[str, np.ndarray]) -> SD:
     return {k: torch.from_numpy(np.asarray(v, dtype=np.float32)) for k, v in sd_np.items()}
+
+
+# --------------------------------------------------------------------------------------------
+# VapGPTMono (vap/model.py:271-393)
+# --------------------------------------------------------------------------------------------
+def encode_va(va: Tensor, sd: SD, va_history: Optional[Tensor] = None) -> Tensor:
+    """VapGPTMono.encode_va (model.py:352-357): LN(va_condition(va) [+ va_cond_history(hist)])."""
+    v = va @ sd["va_condition.weight"].T + sd["va_condition.bias"]
+    if va_history is not None and "va_cond_history.weight" in sd:
+        v = v + va_history @ sd["va_cond_history.weight"].T + sd["va_cond_history.bias"]
+    return layer_norm(v, sd, "va_cond_ln")
+
+
+def forward_mono(waveform: Tensor, va: Tensor, sd: SD, va_history: Optional[Tensor] = None,
+                 num_heads: int = 4) -> Dict[str, Tensor]:
+    """VapGPTMono.forward (model.py:360-393): encoder on one speaker, + encode_va, ar_channel GPT,
+    ar GPT (self attention only), vap_head; "vad" is the va input itself."""
+    assert waveform.shape[1] == 1, f"audio VAP ENCODER: {waveform.shape} != (B, 1, n_samples)"
+    x = encoder(waveform, sd)
+    x = x + encode_va(va, sd, va_history)
+    for l in range(count_layers(sd, "ar_channel")):
+        x = transformer_layer(x, sd, f"ar_channel.layers.{l}", num_heads)
+    for l in range(count_layers(sd, "ar")):
+        x = transformer_layer(x, sd, f"ar.layers.{l}", num_heads)
+    logits = x @ sd["vap_head.weight"].T + sd["vap_head.bias"]
+    return {"logits": logits, "vad": va}
+
+
+def probs_mono(waveform: Tensor, va: Tensor, sd: SD, va_history: Optional[Tensor] = None, num_heads: int = 4,
+               now_lims=(0, 1), future_lims=(2, 3), n_bins: int = 4) -> Dict[str, Tensor]:
+    """VapGPTMono.probs (model.py:325-350): no labels / loss (unlike VapGPT.probs)."""
+    with torch.no_grad():
+        out = forward_mono(waveform, va, sd, va_history, num_heads)
+        pr = out["logits"].softmax(dim=-1)
+        H = (-pr * pr.log2()).sum(dim=-1)
+        p_now = probs_next_speaker_aggregate(pr, now_lims[0], now_lims[-1], n_bins)
+        p_future = probs_next_speaker_aggregate(pr, future_lims[0], future_lims[1], n_bins)
+    return {"probs": pr, "vad": va, "p_now": p_now, "p_future": p_future, "H": H}

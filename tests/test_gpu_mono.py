@@ -1,0 +1,81 @@
+"""VapGPTMono (vap/model.py:271-393) on the engine vs the reference's own outputs
+(tests/golden/mono.npz, tools/gen_golden.py mono) and vs the CPU oracle.
+
+Tolerances: fp32 mode 1e-4 absolute on logits-derived probabilities (logits 2e-4: they are O(10));
+bf16 mode the BF16 tolerances of test_gpu_parity.py."""
+import numpy as np
+import pytest
+import torch
+
+import vap_oracle as O
+from voiceactivityprojection_amd.weights import synthetic_state_dict, synthetic_waveform
+
+pytestmark = pytest.mark.gpu
+
+
+def _mono(precision):
+    from vap.model import VapGPTMono, VapMonoConfig
+
+    m = VapGPTMono(VapMonoConfig(va_history=True, va_history_bins=5), precision=precision)
+    sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed=0, mono=True, va_history_bins=5).items()}
+    m.load_state_dict(sd, strict=True)
+    return m.to("cuda").eval()
+
+
+@pytest.fixture(scope="module")
+def mono32():
+    return _mono("fp32")
+
+
+def test_mono_fp32_vs_reference(mono32, golden):
+    g = golden("mono")
+    w, va, hist = (torch.from_numpy(g[k]).cuda() for k in ("waveform", "va", "va_history"))
+    out = mono32(w, va, hist)
+    assert out["vad"] is va
+    err = float((out["logits"].cpu() - torch.from_numpy(g["logits"])).abs().max())
+    assert err < 2e-4, f"logits {err}"
+    pr = mono32.probs(w, va)  # the reference's probs() passes no history
+    for k, gk in (("probs", "probs_logits_nohist"), ("p_now", "p_now"), ("p_future", "p_future"), ("H", "H")):
+        e = float((pr[k].cpu() - torch.from_numpy(g[gk])).abs().max())
+        assert e < (1e-3 if k == "H" else 1e-4), f"{k}: {e}"
+    assert pr["vad"] is va and "loss" not in pr
+
+
+def test_mono_encode_paths(mono32, golden):
+    g = golden("mono")
+    sd = O.state_dict_to_torch(synthetic_state_dict(seed=0, mono=True, va_history_bins=5))
+    w = torch.from_numpy(g["waveform"])
+    enc = mono32.encode_audio(w.cuda()).cpu()
+    np.testing.assert_allclose(enc.numpy(), O.encoder(w, sd).numpy(), atol=1e-4)
+    va, hist = torch.from_numpy(g["va"]), torch.from_numpy(g["va_history"])
+    ev = mono32.encode_va(va.cuda(), hist.cuda()).cpu()
+    np.testing.assert_allclose(ev.numpy(), O.encode_va(va, sd, hist).numpy(), atol=1e-5)
+
+
+def test_mono_bf16_batch_vs_oracle():
+    m = _mono("bf16")
+    sd = O.state_dict_to_torch(synthetic_state_dict(seed=0, mono=True, va_history_bins=5))
+    B, n = 3, 64000
+    wav = torch.from_numpy(np.stack([synthetic_waveform(50 + i, n, channels=1) for i in range(B)]))
+    T = O.frame_lengths(n)[-1]
+    g = torch.Generator().manual_seed(3)
+    va = (torch.rand(B, T, 2, generator=g) < 0.5).float()
+    hist = torch.rand(B, T, 5, generator=g)
+    got = m.probs(wav.cuda(), va.cuda())
+    ref = O.probs_mono(wav, va, sd)
+    for k, tol in (("probs", 2e-2), ("p_now", 5e-2), ("p_future", 5e-2), ("H", 1.5e-1)):
+        e = float((got[k].cpu() - ref[k]).abs().max())
+        assert e < tol, f"{k}: {e}"
+    lg = m(wav.cuda(), va.cuda(), hist.cuda())["logits"]
+    # batch invariance: each clip alone gives the same logits
+    one = m(wav[1:2].cuda(), va[1:2].cuda(), hist[1:2].cuda())["logits"]
+    assert torch.equal(lg[1:2], one)
+
+
+def test_mono_errors(mono32):
+    with pytest.raises(AssertionError):
+        mono32(torch.zeros(1, 2, 16000, device="cuda"), torch.zeros(1, 50, 2, device="cuda"))
+    with pytest.raises(AssertionError, match="not implemented"):
+        mono32(torch.zeros(1, 1, 16000, device="cuda"), torch.zeros(1, 50, 2, device="cuda"), attention=True)
+    with pytest.raises(RuntimeError):
+        mono32(torch.zeros(1, 1, 16000, device="cuda"), torch.zeros(1, 49, 2, device="cuda"))

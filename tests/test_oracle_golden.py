@@ -117,3 +117,16 @@ def test_oracle_attention_maps_vs_reference(golden):
         assert got.shape == ref.shape, (k, got.shape, ref.shape)
         err = float(np.abs(got - ref).max())
         assert err < 1e-5, f"{k}: {err}"
+
+
+def test_oracle_mono_vs_reference(golden):
+    """VapGPTMono forward (with va_history) and probs (without, as the reference's probs()) of the
+    oracle against the reference's own outputs (tools/gen_golden.py mono)."""
+    g = golden("mono")
+    sd = O.state_dict_to_torch(synthetic_state_dict(seed=0, mono=True, va_history_bins=5))
+    w, va, hist = (torch.from_numpy(g[k]) for k in ("waveform", "va", "va_history"))
+    out = O.forward_mono(w, va, sd, hist)
+    assert float((out["logits"] - torch.from_numpy(g["logits"])).abs().max()) < 1e-4
+    pr = O.probs_mono(w, va, sd)
+    for k, gk in (("probs", "probs_logits_nohist"), ("p_now", "p_now"), ("p_future", "p_future"), ("H", "H")):
+        assert float((pr[k] - torch.from_numpy(g[gk])).abs().max()) < 2e-5, k

@@ -12,6 +12,7 @@ with ``strict=True``.  Outputs land in ``tests/golden/*.npz`` (inputs + expected
 
 Usage:  python tools/gen_golden.py            (takes ~1 min on 8 CPU threads)
         python tools/gen_golden.py attention  (only the attention-map fixture)
+        python tools/gen_golden.py mono       (only the VapGPTMono fixture)
 """
 from __future__ import annotations
 
@@ -203,9 +204,38 @@ def gen_attention():
     print("wrote attention_maps.npz", {k: tuple(v.shape) for k, v in out.items()})
 
 
+def gen_mono():
+    """(h) VapGPTMono (vap/model.py:271-393) with va_history (5 bins): forward + probs of a 2.56 s mono
+    clip with a seeded binary VA track and its history bins."""
+    torch.set_num_threads(8)
+    import_reference(1)
+    from vap.model import VapGPTMono, VapMonoConfig
+
+    model = VapGPTMono(VapMonoConfig(va_history=True, va_history_bins=5))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed=0, mono=True, va_history_bins=5).items()}
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    n = 40960
+    wav = synthetic_waveform(40, n, channels=1)[None]
+    T = 128
+    rng = np.random.default_rng(41)
+    va = (rng.random((1, T, 2)) < 0.4).astype(np.float32)
+    hist = rng.random((1, T, 5)).astype(np.float32)
+    with torch.no_grad():
+        out = model(torch.from_numpy(wav), torch.from_numpy(va), torch.from_numpy(hist))
+        pr = model.probs(torch.from_numpy(wav), torch.from_numpy(va))  # probs() passes no history
+    np.savez_compressed(os.path.join(OUT, "mono.npz"), waveform=wav, va=va, va_history=hist,
+                        logits=out["logits"].numpy(), probs_logits_nohist=pr["probs"].numpy(),
+                        p_now=pr["p_now"].numpy(), p_future=pr["p_future"].numpy(), H=pr["H"].numpy())
+    print("wrote mono.npz", out["logits"].shape)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "attention":
         gen_attention()
+    elif len(sys.argv) > 1 and sys.argv[1] == "mono":
+        gen_mono()
     else:
         main()
         gen_attention()
+        gen_mono()

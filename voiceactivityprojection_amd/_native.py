@@ -22,7 +22,7 @@ KERNEL_CLASS = {"conv0": 1, "conv1": 2, "conv234": 3, "lstm_proj": 4, "lstm_rec"
 class VapDims(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int), ("num_heads", ctypes.c_int), ("channel_layers", ctypes.c_int),
                 ("cross_layers", ctypes.c_int), ("lstm_layers", ctypes.c_int), ("n_bins", ctypes.c_int),
-                ("precision", ctypes.c_int)]
+                ("precision", ctypes.c_int), ("mono", ctypes.c_int), ("va_history_bins", ctypes.c_int)]
 
 
 class NativeLibraryMissing(ImportError):
@@ -44,6 +44,8 @@ _SIGS = {
     "vap_workspace_size": (ctypes.c_int, [_P, ctypes.c_int, _I64, ctypes.POINTER(ctypes.c_size_t)]),
     "vap_forward": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, _P, ctypes.c_size_t, _P]),
     "vap_forward_attention": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "vap_forward_mono": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, _I64, _P, _P, ctypes.c_size_t, _P]),
+    "vap_encode_va": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, _P]),
     "vap_encode": (ctypes.c_int, [_P, _P, ctypes.c_int, _I64, _P, _P, ctypes.c_size_t, _P]),
     "vap_stream_create": (ctypes.c_int, [_P, ctypes.c_int, _I64, _I64, _P, _P]),
     "vap_stream_push": (ctypes.c_int, [_P, _P, _P, _P, _P]),

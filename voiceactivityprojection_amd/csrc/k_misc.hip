@@ -298,8 +298,9 @@ __global__ void add_vec_kernel(const float* a, const float* b, float* out, int n
 
 template <typename T>
 hipError_t launch_conv0(const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
-                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st) {
-  dim3 grid((L0 + 63) / 64, 2 * B);
+                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st,
+                        int nseq) {
+  dim3 grid((L0 + 63) / 64, nseq > 0 ? nseq : 2 * B);
   hipLaunchKernelGGL((conv0_kernel<T>), grid, dim3(256), 0, st, wav, B, N, L0, w0, b0, gamma, beta, out,
                      out_seq_stride);
   return hipGetLastError();
@@ -404,7 +405,7 @@ hipError_t launch_add_vec(const float* a, const float* b, float* out, int n, hip
 
 #define INST(T)                                                                                                       \
   template hipError_t launch_conv0<T>(const float*, int, int64_t, int, const float*, const float*, const float*,       \
-                                      const float*, T*, int64_t, hipStream_t);                                         \
+                                      const float*, T*, int64_t, hipStream_t, int);                                    \
   template hipError_t launch_zero_rows<T>(T*, int, int64_t, int, hipStream_t);                                          \
   template hipError_t launch_layernorm<T>(const float*, int64_t, const float*, const float*, float, T*, T*,           \
                                           hipStream_t);                                                                \
@@ -412,3 +413,51 @@ hipError_t launch_add_vec(const float* a, const float* b, float* out, int n, hip
   template hipError_t launch_pack_conv<T>(const float*, T*, int, int, int, hipStream_t);
 INST(float)
 INST(bf16)
+
+// ------------------------------------------------------------------------------------------
+// VapGPTMono.encode_va (vap/model.py:352-357): LN(va_condition(va) [+ va_cond_history(hist)]),
+// added to the encoder output (model.py:378).  One wave per row, 4 channels per lane.
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void va_cond_kernel(float* __restrict__ x, const float* __restrict__ va,
+                                                      const float* __restrict__ hist, int rows, int bins,
+                                                      const float* __restrict__ Wv, const float* __restrict__ bv,
+                                                      const float* __restrict__ Wh, const float* __restrict__ bh,
+                                                      const float* __restrict__ gam, const float* __restrict__ bet) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float a0 = va[(int64_t)r * 2], a1 = va[(int64_t)r * 2 + 1];
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = lane * 4 + e;
+    float t = fmaf(Wv[c * 2], a0, fmaf(Wv[c * 2 + 1], a1, bv[c]));
+    if (hist) {
+      t += bh[c];
+      for (int k = 0; k < bins; ++k) t = fmaf(Wh[c * bins + k], hist[(int64_t)r * bins + k], t);
+    }
+    v[e] = t;
+  }
+  const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.0f / 256);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) ss += (v[e] - mean) * (v[e] - mean);
+  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / 256) + 1e-5f);
+  float* xr = x + (int64_t)r * 256 + lane * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = lane * 4 + e;
+    xr[e] += (v[e] - mean) * rstd * gam[c] + bet[c];
+  }
+}
+}  // namespace
+
+hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows, int bins, const float* Wv,
+                          const float* bv, const float* Wh, const float* bh, const float* gamma, const float* beta,
+                          hipStream_t st) {
+  if (rows <= 0 || (hist && bins <= 0)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(va_cond_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x, va, hist, rows, bins, Wv, bv, Wh, bh,
+                     gamma, beta);
+  return hipGetLastError();
+}

@@ -69,8 +69,11 @@ struct vap_handle {
   int time_chunks = 4;          // VAP_TIME_CHUNKS (bf16, 1-layer LSTM): pipeline the forward along time
   int tc_streams = 1;           // VAP_TC_STREAMS=2: back ends on their own stream (measured: no gain, kernels fill the GPU)
   bool use_time_chunks() const {
-    return dims.precision == VAP_PRECISION_BF16 && dims.lstm_layers == 1 && time_chunks >= 2;
+    return dims.precision == VAP_PRECISION_BF16 && dims.lstm_layers == 1 && time_chunks >= 2 && !dims.mono;
   }
+  // VapGPTMono (dims.mono): the VA conditioning inputs of the running vap_forward_mono call
+  const float* mono_va = nullptr;
+  const float* mono_hist = nullptr;
   int ensure_streams() {
     if (streams_ready) return VAP_OK;
     for (auto& s : side)
@@ -171,6 +174,22 @@ void add_schema(vap_handle* h) {
       for (const char* n : {"key", "query", "value", "proj"}) add(p + ".mha_cross." + n + ".weight", D * D);
     }
   };
+  if (d.mono) {  // VapGPTMono.init_va_conditioning (vap/model.py:317-323)
+    add("va_condition.weight", D * 2);
+    add("va_condition.bias", D);
+    add("va_cond_ln.weight", D);
+    add("va_cond_ln.bias", D);
+    if (d.va_history_bins > 0) {
+      add("va_cond_history.weight", (int64_t)D * d.va_history_bins);
+      add("va_cond_history.bias", D);
+    }
+    for (int l = 0; l < d.channel_layers; ++l) layer("ar_channel.layers." + std::to_string(l), false);
+    for (int l = 0; l < d.cross_layers; ++l) layer("ar.layers." + std::to_string(l), false);  // plain GPT
+    add("objective.codebook.emb.weight", 256 * 8);
+    add("vap_head.weight", 256 * D);
+    add("vap_head.bias", 256);
+    return;
+  }
   for (int l = 0; l < d.channel_layers; ++l) layer("ar_channel.layers." + std::to_string(l), false);
   for (int l = 0; l < d.cross_layers; ++l) layer("ar.layers." + std::to_string(l), true);
   add("ar.combinator.h0_a.weight", D * D);
@@ -209,10 +228,10 @@ struct Plan {
 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
-Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross_layers = 0) {
+Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross_layers = 0, int ch = 2) {
   Plan p;
   p.B = B;
-  p.S = 2 * B;
+  p.S = ch * B;  // sequences: 2 speakers per clip (VapGPT), 1 (VapGPTMono)
   frame_lengths(N, p.L);
   p.T = (int)p.L[5];
   const int64_t S = p.S, T = p.T;
@@ -255,6 +274,7 @@ Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross
 Plan plan_for(const vap_handle* h, int B, int64_t N) {
   const size_t es = h->dims.precision == VAP_PRECISION_BF16 ? 2 : 4;
   const int nl = h->dims.channel_layers + h->dims.cross_layers;
+  if (h->dims.mono) return make_plan(B, N, es, 0, 0, 1);
   return h->use_time_chunks() ? make_plan(B, N, es, nl, h->dims.cross_layers) : make_plan(B, N, es);
 }
 
@@ -470,9 +490,11 @@ int pack_all(vap_handle* h, hipStream_t st) {
   for (int l = 0; l < h->dims.channel_layers; ++l)
     if ((rc = layer("ar_channel.layers." + std::to_string(l), false))) return rc;
   for (int l = 0; l < h->dims.cross_layers; ++l)
-    if ((rc = layer("ar.layers." + std::to_string(l), true))) return rc;
-  if ((rc = cat("comb_a", {"ar.combinator.h0_a.weight"}))) return rc;
-  if ((rc = cat("comb_b", {"ar.combinator.h0_b.weight"}))) return rc;
+    if ((rc = layer("ar.layers." + std::to_string(l), !h->dims.mono))) return rc;
+  if (!h->dims.mono) {
+    if ((rc = cat("comb_a", {"ar.combinator.h0_a.weight"}))) return rc;
+    if ((rc = cat("comb_b", {"ar.combinator.h0_b.weight"}))) return rc;
+  }
   if ((rc = cat("head", {"vap_head.weight"}))) return rc;
   return VAP_OK;
 }
@@ -482,8 +504,9 @@ int pack_all(vap_handle* h, hipStream_t st) {
 // so a micro-batch of clips is one contiguous sequence range, and the stereo partner of s is s^1.
 struct Range {
   int c0, nc;  // clips [c0, c0+nc)
-  int s0() const { return 2 * c0; }
-  int ns() const { return 2 * nc; }
+  int ch = 2;  // sequences per clip (1: VapGPTMono)
+  int s0() const { return ch * c0; }
+  int ns() const { return ch * nc; }
 };
 
 // bf16 transformer layer on row-panel kernels: LayerNorm fused into the A-panel load of the
@@ -683,7 +706,7 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     Timed tm(h, VAP_K_CONV0, st);
     HIPCHK(launch_conv0<T>(wav + (int64_t)r.s0() * N, r.nc, N, (int)L[0], h->P(g + ".conv0.weight"),
                            h->P(g + ".conv0.bias"), h->P(g + ".batchNorm0.weight"), h->P(g + ".batchNorm0.bias"), X0,
-                           p.s0, st));
+                           p.s0, st, S));
   }
   // conv1..conv4 as implicit GEMMs with ChannelNorm + ReLU epilogue (encoder_components.py:100-103)
   const T* ins[4] = {X0, Xs[0], Xs[1], Xs[2]};
@@ -748,6 +771,13 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
   const int64_t t1 = (int64_t)T_ * D;
   float* X = (float*)(ws + p.X) + r.s0() * t1;
   T* RAW = (T*)(ws + p.RAW) + r.s0() * t1;
+  if (h->dims.mono) {  // VapGPTMono: logits = vap_head(x) (vap/model.py:384-385); no combinator / VAD head
+    Timed tm(h, VAP_K_HEADS, st);
+    HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));  // fp32 -> storage
+    HIPCHK(gemm<T>(gargs(RAW, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, S,
+                         logits + (int64_t)r.c0 * T_ * 256, 256, (int64_t)T_ * 256), st, true));
+    return VAP_OK;
+  }
   float* HC = (float*)(ws + p.HC) + r.c0 * t1;
   T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
   {
@@ -795,18 +825,27 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
     ga.beta = h->P("encoder.downsample.2.ln.bias");
     HIPCHK(gemm<T>(ga, st, true));
   }
-  if (enc_out) {  // EncoderCPC output, (x1, x2) = channel 0 / 1 -> enc_out [2][B][T][256]
+  if (enc_out) {  // EncoderCPC output, (x1, x2) = channel 0 / 1 -> enc_out [2][B][T][256] ([B][T][256] mono)
     const int64_t B = p.B;
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < r.ch; ++c)
       HIPCHK(hipMemcpy2DAsync(enc_out + ((int64_t)c * B + r.c0) * t1, t1 * sizeof(float), X + c * t1,
-                              2 * t1 * sizeof(float), t1 * sizeof(float), r.nc, hipMemcpyDeviceToDevice, st));
+                              r.ch * t1 * sizeof(float), t1 * sizeof(float), r.nc, hipMemcpyDeviceToDevice, st));
     return VAP_OK;
+  }
+  if (h->dims.mono) {  // x = x + encode_va(va, va_history) (vap/model.py:352-357, 378)
+    Timed tm(h, VAP_K_NORM, st);
+    const int bins = h->dims.va_history_bins;
+    const bool hist = bins > 0 && h->mono_hist;
+    HIPCHK(launch_va_cond(X, h->mono_va + (int64_t)r.c0 * T_ * 2, hist ? h->mono_hist + (int64_t)r.c0 * T_ * bins : nullptr,
+                          S * T_, bins, h->P("va_condition.weight"), h->P("va_condition.bias"),
+                          hist ? h->P("va_cond_history.weight") : nullptr, hist ? h->P("va_cond_history.bias") : nullptr,
+                          h->P("va_cond_ln.weight"), h->P("va_cond_ln.bias"), st));
   }
   int rc;
   for (int l = 0; l < h->dims.channel_layers; ++l)
     if ((rc = tr_layer<T>(h, p, ws, "ar_channel.layers." + std::to_string(l), false, r, st, l))) return rc;
   for (int l = 0; l < h->dims.cross_layers; ++l)
-    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), true, r, st, l))) return rc;
+    if ((rc = tr_layer<T>(h, p, ws, "ar.layers." + std::to_string(l), !h->dims.mono, r, st, l))) return rc;
 
   return heads<T>(h, p, ws, r, logits, vadl, st);
 }
@@ -1101,11 +1140,11 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   const int NL = h->dims.lstm_layers;
   int m = h->microbatches < 1 ? 1 : h->microbatches;
   if (m > B) m = B;
-  if (NL > 1 || h->amap_active()) m = 1;  // stacked LSTMs / attention maps: the simple serial schedule
+  if (NL > 1 || h->amap_active() || h->dims.mono) m = 1;  // stacked LSTMs / attention maps / mono: serial
   std::vector<Range> rs;
   for (int i = 0; i < m; ++i) {
     const int c0 = (int)((int64_t)B * i / m), c1 = (int)((int64_t)B * (i + 1) / m);
-    if (c1 > c0) rs.push_back({c0, c1 - c0});
+    if (c1 > c0) rs.push_back({c0, c1 - c0, h->dims.mono ? 1 : 2});
   }
   int rc;
   if constexpr (sizeof(T) == 2) {
@@ -1321,6 +1360,9 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
     return fail(VAP_ERR_INVALID, "bad layer counts");
   if (dims->precision != VAP_PRECISION_FP32 && dims->precision != VAP_PRECISION_BF16)
     return fail(VAP_ERR_INVALID, "bad precision");
+  if (dims->mono != 0 && dims->mono != 1) return fail(VAP_ERR_INVALID, "bad mono flag");
+  if (dims->va_history_bins < 0 || (!dims->mono && dims->va_history_bins))
+    return fail(VAP_ERR_INVALID, "va_history_bins is a VapGPTMono option");
   vap_handle* h = new vap_handle();
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
@@ -1406,6 +1448,7 @@ int vap_workspace_size(const vap_handle* h, int batch, int64_t n_samples, size_t
 int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_samples, float* logits, float* vad_logits,
                 void* workspace, size_t workspace_bytes, void* stream) {
   if (!h || !waveform || !logits || !vad_logits || !workspace) return fail(VAP_ERR_INVALID, "null argument");
+  if (h->dims.mono) return fail(VAP_ERR_INVALID, "mono handle: use vap_forward_mono");
   if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
   if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
   size_t need = 0;
@@ -1431,9 +1474,45 @@ int vap_forward_attention(vap_handle* h, const float* waveform, int batch, int64
   return rc;
 }
 
+int vap_forward_mono(vap_handle* h, const float* waveform, const float* va, const float* va_history, int batch,
+                     int64_t n_samples, float* logits, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!h || !waveform || !va || !logits || !workspace) return fail(VAP_ERR_INVALID, "null argument");
+  if (!h->dims.mono) return fail(VAP_ERR_INVALID, "vap_forward_mono needs a handle created with dims.mono = 1");
+  if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
+  if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  size_t need = 0;
+  int rc = vap_workspace_size(h, batch, n_samples, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) return fail(VAP_ERR_INVALID, "workspace too small: need " + std::to_string(need));
+  h->mono_va = va;
+  h->mono_hist = va_history;
+  rc = h->dims.precision == VAP_PRECISION_BF16
+           ? run_forward<bf16>(h, waveform, batch, n_samples, logits, nullptr, (unsigned char*)workspace,
+                               (hipStream_t)stream)
+           : run_forward<float>(h, waveform, batch, n_samples, logits, nullptr, (unsigned char*)workspace,
+                                (hipStream_t)stream);
+  h->mono_va = h->mono_hist = nullptr;
+  return rc;
+}
+
+int vap_encode_va(vap_handle* h, const float* va, const float* va_history, int rows, float* out, void* stream) {
+  if (!h || !va || !out || rows <= 0) return fail(VAP_ERR_INVALID, "bad argument");
+  if (!h->dims.mono) return fail(VAP_ERR_INVALID, "vap_encode_va needs a handle created with dims.mono = 1");
+  if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
+  const int bins = h->dims.va_history_bins;
+  const bool hist = bins > 0 && va_history;
+  HIPCHK(hipMemsetAsync(out, 0, (size_t)rows * D * sizeof(float), (hipStream_t)stream));
+  HIPCHK(launch_va_cond(out, va, hist ? va_history : nullptr, rows, bins, h->P("va_condition.weight"),
+                        h->P("va_condition.bias"), hist ? h->P("va_cond_history.weight") : nullptr,
+                        hist ? h->P("va_cond_history.bias") : nullptr, h->P("va_cond_ln.weight"),
+                        h->P("va_cond_ln.bias"), (hipStream_t)stream));
+  return VAP_OK;
+}
+
 int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t hop_samples, void* stream,
                       vap_stream** out) {
   if (!h || !out) return fail(VAP_ERR_INVALID, "null argument");
+  if (h->dims.mono) return fail(VAP_ERR_UNSUPPORTED, "streaming is a VapGPT (stereo) path");
   if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
   if (batch <= 0 || window_samples <= 0 || hop_samples <= 0 || hop_samples > window_samples)
     return fail(VAP_ERR_INVALID, "bad batch / window / hop");

@@ -28,10 +28,17 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
 template <typename TOut>
 hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st);
 
-// conv0 (1 -> 256, k10 s5 p3) + ChannelNorm + ReLU, time-major output with pad rows.
+// conv0 (1 -> 256, k10 s5 p3) + ChannelNorm + ReLU, time-major output with pad rows; 2B sequences
+// (stereo clips) or nseq when given (mono: one sequence per clip).
 template <typename T>
 hipError_t launch_conv0(const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
-                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st);
+                        const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st,
+                        int nseq = -1);
+// VapGPTMono VA conditioning (vap/model.py:317-323, 352-357): x[r] += LayerNorm(Wv va[r] + bv
+// (+ Wh hist[r] + bh)) for each of `rows` 256-wide rows; va [rows][2], hist [rows][bins] or NULL.
+hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows, int bins, const float* Wv,
+                          const float* bv, const float* Wh, const float* bh, const float* gamma, const float* beta,
+                          hipStream_t st);
 
 // Zero `rows` rows of width 256 at `base + s*seq_stride` for every sequence (pad rows).
 template <typename T>

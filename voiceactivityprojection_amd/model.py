@@ -109,16 +109,19 @@ class VapGPT(nn.Module):
         self._ws: Optional[Tensor] = None
 
     # ------------------------------------------------------------------ parameters / state dict
+    def _schema_kw(self) -> dict:
+        return {}
+
     def _schema(self, lstm_layers: int):
         c = self.conf
         return _schema(dim=c.dim, channel_layers=c.channel_layers, cross_layers=c.cross_layers,
-                       num_heads=c.num_heads, lstm_layers=lstm_layers, n_bins=len(c.bin_times))
+                       num_heads=c.num_heads, lstm_layers=lstm_layers, n_bins=len(c.bin_times), **self._schema_kw())
 
     def _build_params(self, lstm_layers: int):
         c = self.conf
         init = synthetic_state_dict(seed=0, dim=c.dim, channel_layers=c.channel_layers,
                                     cross_layers=c.cross_layers, num_heads=c.num_heads,
-                                    lstm_layers=lstm_layers, n_bins=len(c.bin_times))
+                                    lstm_layers=lstm_layers, n_bins=len(c.bin_times), **self._schema_kw())
         for key, shape in self._schema(lstm_layers):
             if key == "objective.codebook.emb.weight":
                 continue  # owned by ObjectiveVAP.codebook.emb
@@ -190,8 +193,10 @@ class VapGPT(nn.Module):
         lib = N.lib()
         self._free_handle()
         c = self.conf
+        kw = self._schema_kw()
         dims = N.VapDims(c.dim, c.num_heads, c.channel_layers, c.cross_layers, self.lstm_layers,
-                         len(c.bin_times), N.PRECISION[self.precision])
+                         len(c.bin_times), N.PRECISION[self.precision], int(kw.get("mono", False)),
+                         int(kw.get("va_history_bins", 0)))
         h = ctypes.c_void_p()
         N.check(lib.vap_create(ctypes.byref(dims), ctypes.byref(h)), "vap_create")
         self._handle = h
@@ -340,6 +345,133 @@ def _stream(self, batch: int, context_time: float = 10.0, hop_time: float = 1.0,
 
 
 VapGPT.stream = _stream
+
+
+@dataclass
+class VapMonoConfig:
+    """vap/model.py:82-124 (same fields and defaults)."""
+    sample_rate: int = 16_000
+    frame_hz: int = 50
+    bin_times: List[float] = field(default_factory=lambda: BIN_TIMES)
+    mono: bool = True
+    va_history: bool = False
+    va_history_bins: int = 5
+
+    freeze_encoder: bool = True
+    load_pretrained: bool = True
+
+    dim: int = 256
+    channel_layers: int = 1
+    cross_layers: int = 3
+    num_heads: int = 4
+    dropout: float = 0.1
+
+    # the reference's argparse helpers iterate and build VapConfig (model.py:101-124); kept as is
+    add_argparse_args = staticmethod(VapConfig.add_argparse_args)
+    args_to_conf = staticmethod(VapConfig.args_to_conf)
+
+
+class VapGPTMono(VapGPT):
+    """vap/model.py:271-393 on the MI355X engine: one speaker's CPC encoder + VA conditioning
+    (``va_condition`` Linear(2, dim) -> ``va_cond_ln``, plus ``va_cond_history`` when
+    ``conf.va_history``), ``ar_channel`` and ``ar`` plain GPT stacks, ``vap_head``.  Same state-dict
+    keys; forward / probs / encode_audio / encode_va with the reference's signatures."""
+
+    def __init__(self, conf: Optional[VapMonoConfig] = None, precision: Optional[str] = None, lstm_layers: int = 1):
+        super().__init__(conf if conf is not None else VapMonoConfig(), precision, lstm_layers)
+
+    def _schema_kw(self) -> dict:
+        c = self.conf
+        return {"mono": True, "va_history_bins": int(c.va_history_bins) if c.va_history else 0}
+
+    def encode_audio(self, audio: Tensor) -> Tensor:
+        """model.py:359-363: (B, 1, N) -> (B, T, 256)."""
+        assert audio.shape[1] == 1, f"audio VAP ENCODER: {audio.shape} != (B, 1, n_samples)"
+        if not audio.is_cuda:
+            raise RuntimeError("VapGPTMono (MI355X engine) runs on HIP devices only (there is no CPU fallback)")
+        audio = audio.float().contiguous()
+        B, _, n = audio.shape
+        T = N.frame_lengths(n)[-1]
+        h = self._native(audio.device)
+        ws = self._workspace(h, B, n, audio.device)
+        out = torch.empty(B, T, self.conf.dim, device=audio.device, dtype=torch.float32)
+        N.check(N.lib().vap_encode(h, audio.data_ptr(), B, n, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   N.stream_ptr(audio.device)), "vap_encode")
+        return out
+
+    def encode_va(self, va: Tensor, va_history: Optional[Tensor] = None) -> Tensor:
+        """model.py:352-357: LN(va_condition(va) [+ va_cond_history(va_history)])."""
+        if not va.is_cuda:
+            raise RuntimeError("VapGPTMono (MI355X engine) runs on HIP devices only (there is no CPU fallback)")
+        va = va.float().contiguous()
+        hist = self._history(va_history, va)
+        rows = va.numel() // 2
+        out = torch.empty(*va.shape[:-1], self.conf.dim, device=va.device, dtype=torch.float32)
+        h = self._native(va.device)
+        N.check(N.lib().vap_encode_va(h, va.data_ptr(), hist.data_ptr() if hist is not None else None, rows,
+                                      out.data_ptr(), N.stream_ptr(va.device)), "vap_encode_va")
+        return out
+
+    def _history(self, va_history: Optional[Tensor], va: Tensor) -> Optional[Tensor]:
+        if not (self.conf.va_history and va_history is not None):
+            return None  # model.py:355: only with conf.va_history and a history given
+        hist = va_history.to(device=va.device, dtype=torch.float32).contiguous()
+        if hist.shape[:-1] != va.shape[:-1] or hist.shape[-1] != self.conf.va_history_bins:
+            raise RuntimeError(f"va_history {tuple(hist.shape)} does not match va {tuple(va.shape)} "
+                               f"x {self.conf.va_history_bins} bins")
+        return hist
+
+    def forward(self, waveform: Tensor, va: Tensor, va_history: Optional[Tensor] = None,
+                attention: bool = False) -> Dict[str, Tensor]:
+        """model.py:365-393 -> {"logits": (B, T, 256), "vad": va}."""
+        assert not attention, "Attention Mono model is not implemented"
+        assert waveform.shape[1] == 1, f"audio VAP ENCODER: {waveform.shape} != (B, 1, n_samples)"
+        if not waveform.is_cuda:
+            raise RuntimeError("VapGPTMono (MI355X engine) runs on HIP devices only: move the model and the "
+                               "waveform to 'cuda' (there is no CPU fallback)")
+        waveform = waveform.float().contiguous()
+        B, _, n = waveform.shape
+        T = N.frame_lengths(n)[-1]
+        if T <= 0:
+            raise RuntimeError(f"waveform of {n} samples is too short for one frame")
+        if tuple(va.shape) != (B, T, 2):
+            raise RuntimeError(f"va {tuple(va.shape)} must be (B, T, 2) = ({B}, {T}, 2) for this waveform")
+        dev = waveform.device
+        vad = va.to(device=dev, dtype=torch.float32).contiguous()
+        hist = self._history(va_history, vad)
+        h = self._native(dev)
+        ws = self._workspace(h, B, n, dev)
+        logits = torch.empty(B, T, self.objective.n_classes, device=dev, dtype=torch.float32)
+        N.check(N.lib().vap_forward_mono(h, waveform.data_ptr(), vad.data_ptr(),
+                                         hist.data_ptr() if hist is not None else None, B, n, logits.data_ptr(),
+                                         ws.data_ptr(), ws.numel(), N.stream_ptr(dev)), "vap_forward_mono")
+        return {"logits": logits, "vad": va}
+
+    @torch.no_grad()
+    def probs(self, waveform: Tensor, vad: Tensor, now_lims: List[int] = [0, 1],
+              future_lims: List[int] = [2, 3]) -> Dict[str, Tensor]:
+        """model.py:325-350: probs, vad (the argument), p_now, p_future, H -- no labels / loss."""
+        out = self(waveform, vad)
+        logits = out["logits"]
+        B, T, C = logits.shape
+        dev = logits.device
+        probs = torch.empty_like(logits)
+        p_now = torch.empty(B, T, 2, device=dev)
+        p_future = torch.empty(B, T, 2, device=dev)
+        H = torch.empty(B, T, device=dev)
+        sig = torch.empty(B, T, 2, device=dev)  # vap_probs' sigmoid(vad) slot; the mono model returns vad itself
+        zeros = torch.zeros(B, T, 2, device=dev)
+        N.check(N.lib().vap_probs(logits.data_ptr(), zeros.data_ptr(), B, T, self.objective.n_bins,
+                                  now_lims[0], now_lims[-1], future_lims[0], future_lims[1], probs.data_ptr(),
+                                  sig.data_ptr(), p_now.data_ptr(), p_future.data_ptr(), H.data_ptr(),
+                                  N.stream_ptr(dev)), "vap_probs")
+        return {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H}
+
+    def vad(self, *args, **kwargs):
+        raise AttributeError("VapGPTMono has no VAD head (vap/model.py:271-393)")
+
+    def stream(self, *args, **kwargs):
+        raise NotImplementedError("streaming is a VapGPT (stereo) path")
 
 
 class VAPModel(VapGPT):

@@ -86,8 +86,10 @@ def bin_frames(bin_times, frame_hz) -> List[int]:
 
 
 def schema(dim: int = 256, channel_layers: int = 1, cross_layers: int = 3, num_heads: int = 4,
-           lstm_layers: int = 1, n_bins: int = 4, cpc_dim: int = 256) -> List[Tuple[str, Tuple[int, ...]]]:
-    """Ordered (key, shape) list == ``VapGPT(conf).state_dict()`` of the reference."""
+           lstm_layers: int = 1, n_bins: int = 4, cpc_dim: int = 256, mono: bool = False,
+           va_history_bins: int = 0) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Ordered (key, shape) list == ``VapGPT(conf).state_dict()`` of the reference, or with ``mono``
+    ``VapGPTMono(VapMonoConfig(va_history=va_history_bins > 0)).state_dict()`` (vap/model.py:271-323)."""
     C = cpc_dim
     out: List[Tuple[str, Tuple[int, ...]]] = []
     g = "encoder.encoder.gEncoder"
@@ -115,6 +117,19 @@ def schema(dim: int = 256, channel_layers: int = 1, cross_layers: int = 3, num_h
             r += [(f"{prefix}.mha_cross.{n}.weight", (dim, dim)) for n in ("key", "query", "value", "proj")]
         return r
 
+    nb = 2 * n_bins
+    if mono:  # init_va_conditioning (model.py:317-323), plain GPT stacks, vap_head
+        out += [("va_condition.weight", (dim, 2)), ("va_condition.bias", (dim,)),
+                ("va_cond_ln.weight", (dim,)), ("va_cond_ln.bias", (dim,))]
+        if va_history_bins:
+            out += [("va_cond_history.weight", (dim, va_history_bins)), ("va_cond_history.bias", (dim,))]
+        for l in range(channel_layers):
+            out += layer(f"ar_channel.layers.{l}", False)
+        for l in range(cross_layers):
+            out += layer(f"ar.layers.{l}", False)
+        out += [("objective.codebook.emb.weight", (2**nb, nb)),
+                ("vap_head.weight", (2**nb, dim)), ("vap_head.bias", (2**nb,))]
+        return out
     for l in range(channel_layers):
         out += layer(f"ar_channel.layers.{l}", False)
     for l in range(cross_layers):
@@ -154,9 +169,9 @@ def synthetic_state_dict(seed: int = 0, **schema_kw) -> Dict[str, np.ndarray]:
             v = np.asarray(alibi_slopes(heads), dtype=np.float32)
         elif key == "objective.codebook.emb.weight":
             v = code_vectors(shape[1])
-        elif ("batchNorm" in key or ".ln" in key or "ln_" in key) and leaf == "weight":
+        elif ("batchNorm" in key or ".ln" in key or "ln_" in key or "_ln." in key) and leaf == "weight":
             v = 1.0 + 0.2 * uniform(key, n, seed)
-        elif ("batchNorm" in key or ".ln" in key or "ln_" in key) and leaf == "bias":
+        elif ("batchNorm" in key or ".ln" in key or "ln_" in key or "_ln." in key) and leaf == "bias":
             v = 0.1 * uniform(key, n, seed)
         elif "gAR" in key:
             v = uniform(key, n, seed) / np.float32(16.0)  # nn.LSTM default U(-1/sqrt(H), 1/sqrt(H))
