@@ -120,6 +120,12 @@ int vap_stream_push(vap_stream* s, const float* hop_audio, float* logits, float*
 /* frames T of a window, window / hop samples, conv4 rows carried over per push, current window (device). */
 int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, int64_t* hop_samples,
                     int64_t* reused_rows, const float** window);
+/* hipGraph replay of steady-state pushes (bf16 carry-over streams; VAP_STREAM_GRAPH=0 disables): the
+ * caller-stream part of a push is captured once per (gate-ring offset, window buffer, output
+ * pointers) state and replayed; the recurrence launch stays eager on a side stream.  Reports the
+ * graphs captured, the replays so far and the hand-off error word (1 if a flag wait timed out;
+ * synchronous). */
+int vap_stream_graphs(vap_stream* s, int* graphs, int64_t* replays, int* handoff_error);
 /* Window back to zeros; the next push recomputes every row. */
 int vap_stream_reset(vap_stream* s, void* stream);
 void vap_stream_destroy(vap_stream* s);

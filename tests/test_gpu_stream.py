@@ -58,6 +58,16 @@ def test_stream_bit_identical_bf16(m16):
     and 11 (every row has been carried over at least once)."""
     st, _ = _run(m16, 3, 160000, 16000, 12, {0, 1, 9, 11})
     assert st.reused_rows > 800, st.reused_rows  # 10 s window: conv4 rows [1, 899) carried over
+    g = st.graph_info()  # pushes 1.. ran as captured hipGraphs (one per gate-ring state)
+    assert g["replays"] == 11 and g["graphs"] == 10 and g["handoff_error"] == 0, g
+
+
+def test_stream_graph_replays_bit_identical(m16):
+    """Every captured state replayed at least once more (the ring state repeats every 10 pushes):
+    replayed graphs stay bit-identical to a full forward of the window."""
+    st, _ = _run(m16, 2, 160000, 16000, 24, {12, 21, 23}, seed=300)
+    g = st.graph_info()
+    assert g["graphs"] == 10 and g["replays"] == 23 and g["handoff_error"] == 0, g
 
 
 def test_stream_bit_identical_fp32(m32):

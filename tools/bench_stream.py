@@ -4,7 +4,8 @@ hop; one push = one step.  Metric: NEW audio-seconds per second (B x hop per ste
 
     python tools/bench_stream.py [--streams 128] [--steps 10] [--warmup 11]
 
-VAP_STREAM_REUSE=0 disables the CPC conv-row carry-over (full recompute per push) for an A/B.
+VAP_STREAM_REUSE=0 disables the CPC conv-row carry-over (full recompute per push) for an A/B;
+VAP_STREAM_GRAPH=0 issues every push eagerly instead of replaying its captured hipGraph.
 Inputs: the seeded synthetic waveform generator (no dataset), bf16, weights random-init.
 """
 import argparse
@@ -41,15 +42,19 @@ def main():
         st.push(audio[..., k * hop:(k + 1) * hop])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     for k in range(args.warmup, args.warmup + args.steps):
         out = st.push(audio[..., k * hop:(k + 1) * hop])
+    c1 = time.process_time()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    host_ms = (c1 - c0) / args.steps * 1e3
     print(json.dumps({"metric": "new audio-seconds/sec (streaming, 1 s hop / 10 s window)",
                       "value": round(B * 1.0 / dt, 1), "unit": "audio-s/s", "ms_per_step": round(dt * 1e3, 3),
                       "streams": B, "steps": args.steps, "reused_rows": st.reused_rows, "frames": st.frames,
                       "dtype": args.precision, "data": "synthetic",
-                      "window_audio_s_per_s": round(B * 10.0 / dt, 1)}))
+                      "window_audio_s_per_s": round(B * 10.0 / dt, 1),
+                      "host_cpu_ms_per_push": round(host_ms, 3), "graph": st.graph_info()}))
 
 
 if __name__ == "__main__":

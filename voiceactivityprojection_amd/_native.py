@@ -51,6 +51,7 @@ _SIGS = {
     "vap_stream_push": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "vap_stream_info": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "vap_stream_reset": (ctypes.c_int, [_P, _P]),
+    "vap_stream_graphs": (ctypes.c_int, [_P, _P, _P, _P]),
     "vap_stream_destroy": (None, [_P]),
     "vap_probs": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P]),

@@ -461,3 +461,35 @@ hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows
                      gamma, beta);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------
+// Stream-ordered flag hand-offs as kernels (graph-capturable replacements of hipStreamWriteValue32 /
+// hipStreamWaitValue32 for the captured streaming push): a store of v to *p after the preceding
+// work, and a one-lane bounded spin until *p >= v (~2 s, then the error word is set and the stream
+// runs on, so a lost flag never hangs the device).
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ void flag_set_kernel(unsigned* p, unsigned v) {
+  if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void wait_geq_kernel(const unsigned* p, unsigned v, unsigned* err) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+    __builtin_amdgcn_s_sleep(8);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz: 2 s
+      if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+}  // namespace
+
+hipError_t launch_flag_set(unsigned* p, unsigned v, hipStream_t st) {
+  hipLaunchKernelGGL(flag_set_kernel, dim3(1), dim3(64), 0, st, p, v);
+  return hipGetLastError();
+}
+hipError_t launch_wait_geq(const unsigned* p, unsigned v, unsigned* err, hipStream_t st) {
+  hipLaunchKernelGGL(wait_geq_kernel, dim3(1), dim3(64), 0, st, p, v, err);
+  return hipGetLastError();
+}

@@ -7,7 +7,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -983,7 +985,7 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
 // Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
 // every transformer layer on the chunk's frames; then heads over all clips and the join.
 int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& sy, unsigned char* ws, float* logits,
-                float* vadl, hipStream_t st) {
+                float* vadl, hipStream_t st, const unsigned* kernel_expect = nullptr, bool join = true) {
   using T = bf16;
   const int S = p.S, T_ = p.T;
   const int64_t t1 = (int64_t)T_ * D;
@@ -1000,7 +1002,10 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
   int rc;
   for (int c = 0; c < t.nch; ++c) {
     const int f0 = t.fb[c], f1 = t.fb[c + 1];
-    HIPCHK(hipStreamWaitValue32(bst, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
+    if (kernel_expect)  // captured streaming push: the hand-off as a kernel (graph-capturable)
+      HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bst));
+    else
+      HIPCHK(hipStreamWaitValue32(bst, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
     {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
       Timed tm(h, VAP_K_DOWNSAMPLE, bst);
       GemmArgs ga = gargs(Hf + (int64_t)f0 * 2 * D, 2 * D, p.sh, h->W<T>("down"), 5 * D, D,
@@ -1018,6 +1023,7 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst))) return rc;
   }
   if ((rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst))) return rc;
+  if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
   if (bst != st) {
@@ -1263,14 +1269,128 @@ struct vap_stream {
   int64_t pushes = 0;
   int64_t keep0 = 0, keep1 = 0;  // conv4 rows [keep0, keep1) carried over from the previous window
   bool reuse = false;
+  // hipGraph-captured steady-state pushes (SURVEY config C5): the caller-stream part of a push (the
+  // roll, the new rows' conv stack, the ready flags, the back end) is captured once per
+  // (gate-ring offset, window buffer, output pointers) state -- the state repeats with period
+  // L4 / gcd(L4, hop rows) pushes -- and replayed; the persistent recurrence launch stays eager on
+  // the side stream, so the graph never depends on the runtime running its branches concurrently.
+  bool graph = false;            // VAP_STREAM_GRAPH=0 disables
+  float* hop_buf = nullptr;      // staging for the new hop (graph nodes read a fixed address)
+  unsigned* gsync = nullptr;     // own ready[16] / done[16] / error, zeroed every push (epoch 1)
+  struct GKey {
+    int64_t off;
+    int cur;
+    const void* lg;
+    const void* vd;
+    bool operator<(const GKey& o) const {
+      return std::tie(off, cur, lg, vd) < std::tie(o.off, o.cur, o.lg, o.vd);
+    }
+  };
+  std::map<GKey, hipGraphExec_t> graphs;
+  int64_t graph_replays = 0;
+  hipStream_t cap = nullptr;  // capture stream (the caller's may be the legacy null stream, which cannot capture)
   ~vap_stream() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    if (cap) (void)hipStreamDestroy(cap);
     (void)hipFree(ws);
     for (int i = 0; i < 2; ++i) (void)hipFree(win[i]);
     (void)hipFree(gx);
+    (void)hipFree(hop_buf);
+    (void)hipFree(gsync);
   }
 };
 
 namespace {
+
+// Caller-stream part of a steady-state push (captured into a hipGraph by stream_push_graph): roll the
+// staged hop into window buffer nxt, the new rows' conv stack + gate projections with the ready
+// flags as kernels, then the back end waiting on the recurrence's done counters with wait kernels.
+int stream_main_graph(vap_stream* s, const TcSched& t, const LstmSync& sy, const unsigned* expect, int64_t off,
+                      int nxt, float* logits, float* vadl, hipStream_t st) {
+  vap_handle* h = s->h;
+  const Plan& p = s->p;
+  const int S = p.S;
+  const int64_t W = s->W, hop = s->hop, L4 = p.L[4];
+  HIPCHK(hipMemcpy2DAsync(s->win[nxt], W * sizeof(float), s->win[1 - nxt] + hop, W * sizeof(float),
+                          (W - hop) * sizeof(float), S, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpy2DAsync(s->win[nxt] + (W - hop), W * sizeof(float), s->hop_buf, hop * sizeof(float),
+                          hop * sizeof(float), S, hipMemcpyDeviceToDevice, st));
+  const float* wav = s->win[nxt];
+  int rc, published = 0;
+  auto publish = [&](int64_t rows_ready) -> int {
+    while (published < t.nch && t.seq_end[published] <= rows_ready)
+      HIPCHK(launch_flag_set((unsigned*)sy.ready + published++, sy.epoch, st));
+    return VAP_OK;
+  };
+  if (s->keep0 > 0 && (rc = conv_rows(h, p, wav, W, s->ws, s->gx, 0, s->keep0, st, off))) return rc;
+  if ((rc = publish(s->keep1))) return rc;
+  if ((rc = conv_rows(h, p, wav, W, s->ws, s->gx, s->keep1, L4, st, off))) return rc;
+  if ((rc = publish(L4))) return rc;
+  return tc_back_end(h, p, t, sy, s->ws, logits, vadl, st, expect, /*join=*/false);
+}
+
+int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, float* vadl, hipStream_t st) {
+  vap_handle* h = s->h;
+  const Plan& p = s->p;
+  const int S = p.S;
+  const int nxt = 1 - s->cur;
+  const int64_t L4 = p.L[4];
+  const int64_t off = (s->gx_off + s->hop_rows) % L4;
+  const TcSched t = tc_schedule(h, p);
+  // eager: stage the hop, zero the hand-off words, start the recurrence on the side stream
+  HIPCHK(hipMemcpyAsync(s->hop_buf, hop_audio, (size_t)S * s->hop * sizeof(float), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemsetAsync(s->gsync, 0, (2 * vap_handle::MAXMB + 1) * sizeof(unsigned), st));
+  LstmSync sy{};
+  sy.gx_off = (int)off;
+  sy.ready = s->gsync;
+  sy.done = s->gsync + vap_handle::MAXMB;
+  sy.error = s->gsync + 2 * vap_handle::MAXMB;
+  sy.epoch = 1;
+  sy.nr = t.nch;
+  sy.time_mode = 1;
+  for (int c = 0; c < t.nch; ++c) sy.seq_end[c] = t.seq_end[c];
+  unsigned expect[vap_handle::MAXMB];
+  for (int c = 0; c < t.nch; ++c) expect[c] = (unsigned)((S + 15) / 16);  // launch_lstm_resident: 16 sequences / WG
+  hipStream_t side = h->side[0];
+  hipEvent_t fork = h->next_fork_event();
+  HIPCHK(hipEventRecord(fork, st));
+  HIPCHK(hipStreamWaitEvent(side, fork, 0));
+  HIPCHK(launch_lstm_resident(s->gx, S, (int)L4, h->W<bf16>("whh_l0"), (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy));
+  // captured: everything else on the caller's stream
+  const vap_stream::GKey key{off, nxt, logits, vadl};
+  auto it = s->graphs.find(key);
+  if (it == s->graphs.end()) {
+    if (s->graphs.size() >= 32) {  // a state cycle this long is not worth caching: run the part eagerly
+      int rc = stream_main_graph(s, t, sy, expect, off, nxt, logits, vadl, st);
+      if (rc) return rc;
+    } else {
+      HIPCHK(hipStreamBeginCapture(s->cap, hipStreamCaptureModeThreadLocal));
+      const int rc = stream_main_graph(s, t, sy, expect, off, nxt, logits, vadl, s->cap);
+      hipGraph_t g = nullptr;
+      const hipError_t ec = hipStreamEndCapture(s->cap, &g);
+      if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      if (ec != hipSuccess) return fail(VAP_ERR_HIP, std::string("stream capture: ") + hipGetErrorString(ec));
+      hipGraphExec_t ex = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ei != hipSuccess) return fail(VAP_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+      it = s->graphs.emplace(key, ex).first;
+    }
+  }
+  if (it != s->graphs.end()) {
+    HIPCHK(hipGraphLaunch(it->second, st));
+    ++s->graph_replays;
+  }
+  HIPCHK(hipEventRecord(h->mb_ev[0], side));  // join: the recurrence launch has retired
+  HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
+  s->gx_off = off;
+  s->cur = nxt;
+  ++s->pushes;
+  return VAP_OK;
+}
 
 int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vadl, hipStream_t st) {
   vap_handle* h = s->h;
@@ -1278,6 +1398,8 @@ int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad
   const int S = p.S;
   const int nxt = 1 - s->cur;
   const int64_t W = s->W, hop = s->hop, L4 = p.L[4];
+  if (s->graph && s->reuse && s->pushes > 0 && s->keep1 > s->keep0 && h->timing_cls == 0 && h->tc_streams < 2)
+    return stream_push_graph(s, hop_audio, logits, vadl, st);
   // roll: window[:, :W-hop] = old window[:, hop:], window[:, W-hop:] = the new samples
   HIPCHK(hipMemcpy2DAsync(s->win[nxt], W * sizeof(float), s->win[s->cur] + hop, W * sizeof(float),
                           (W - hop) * sizeof(float), S, hipMemcpyDeviceToDevice, st));
@@ -1559,6 +1681,13 @@ int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t 
     }
     if (launch_zero_rows<bf16>((bf16*)(s->ws + p.H0), S, p.sh, 4, st) != hipSuccess) return bail("zero rows");
   }
+  s->graph = s->reuse;
+  if (const char* e = getenv("VAP_STREAM_GRAPH")) s->graph = s->graph && atoi(e) != 0;
+  if (s->graph) {
+    if (hipMalloc(&s->hop_buf, (size_t)S * hop_samples * sizeof(float)) != hipSuccess) return bail("hop staging");
+    if (hipMalloc(&s->gsync, (2 * vap_handle::MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return bail("sync words");
+    if (hipStreamCreateWithFlags(&s->cap, hipStreamNonBlocking) != hipSuccess) return bail("capture stream");
+  }
   if (stream_zero(s, st)) return bail("zero window");
   if (hipStreamSynchronize(st) != hipSuccess) return bail("sync");
   *out = s;
@@ -1578,6 +1707,18 @@ int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, i
   if (hop_samples) *hop_samples = s->hop;
   if (reused_rows) *reused_rows = s->reuse ? s->keep1 - s->keep0 : 0;
   if (window) *window = s->win[s->cur];
+  return VAP_OK;
+}
+
+int vap_stream_graphs(vap_stream* s, int* graphs, int64_t* replays, int* handoff_error) {
+  if (!s) return fail(VAP_ERR_INVALID, "null stream");
+  if (graphs) *graphs = (int)s->graphs.size();
+  if (replays) *replays = s->graph_replays;
+  if (handoff_error) {
+    unsigned e = 0;
+    if (s->gsync) HIPCHK(hipMemcpy(&e, s->gsync + 2 * vap_handle::MAXMB, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *handoff_error = (int)e;
+  }
   return VAP_OK;
 }
 

@@ -34,6 +34,9 @@ template <typename T>
 hipError_t launch_conv0(const float* wav, int B, int64_t N, int L0, const float* w0, const float* b0,
                         const float* gamma, const float* beta, T* out, int64_t out_seq_stride, hipStream_t st,
                         int nseq = -1);
+// graph-capturable stream hand-offs (streaming push): *p = v after the preceding work; wait until *p >= v
+hipError_t launch_flag_set(unsigned* p, unsigned v, hipStream_t st);
+hipError_t launch_wait_geq(const unsigned* p, unsigned v, unsigned* err, hipStream_t st);
 // VapGPTMono VA conditioning (vap/model.py:317-323, 352-357): x[r] += LayerNorm(Wv va[r] + bv
 // (+ Wh hist[r] + bh)) for each of `rows` 256-wide rows; va [rows][2], hist [rows][bins] or NULL.
 hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows, int bins, const float* Wv,

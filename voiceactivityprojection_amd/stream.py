@@ -57,6 +57,17 @@ class VapStream:
         if self.hop_frames > self.frames:
             raise ValueError("hop longer than the window's frames")
         self.pushes = 0
+        # persistent outputs: the engine replays a captured hipGraph per state, whose nodes write
+        # fixed addresses (vap_stream_graphs)
+        self._logits = torch.empty(self.batch, self.frames, 256, device=device)
+        self._vad_logits = torch.empty(self.batch, self.frames, 2, device=device)
+
+    def graph_info(self) -> Dict[str, int]:
+        """hipGraph replay state: graphs captured, pushes replayed, hand-off error word (synchronous)."""
+        g, r, e = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int()
+        N.check(N.lib().vap_stream_graphs(self._s, ctypes.byref(g), ctypes.byref(r), ctypes.byref(e)),
+                "vap_stream_graphs")
+        return {"graphs": g.value, "replays": r.value, "handoff_error": e.value}
 
     def _check_handle(self):
         if self._s is None:
@@ -77,8 +88,7 @@ class VapStream:
         audio = audio.to(device=self.device, dtype=torch.float32).contiguous()
         B, T = self.batch, self.frames
         dev = self.device
-        logits = torch.empty(B, T, 256, device=dev)
-        vad_logits = torch.empty(B, T, 2, device=dev)
+        logits, vad_logits = self._logits, self._vad_logits
         st = N.stream_ptr(dev)
         N.check(N.lib().vap_stream_push(self._s, audio.data_ptr(), logits.data_ptr(), vad_logits.data_ptr(), st),
                 "vap_stream_push")
@@ -94,7 +104,7 @@ class VapStream:
                                   H.data_ptr(), st), "vap_probs")
         out = {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H}
         if full:
-            out["logits"], out["vad_logits"] = logits, vad_logits
+            out["logits"], out["vad_logits"] = logits.clone(), vad_logits.clone()
             return out
         f = self.hop_frames
         return {k: v[:, -f:] for k, v in out.items()}
