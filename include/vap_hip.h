@@ -193,8 +193,17 @@ int vap_test_pack_weight(const void* W, void* out, int N, int K, void* stream);
 int vap_test_ffn_packed(float* x, int M, const void* W1p, const void* W2p, const float* gamma, const float* beta,
                         void* stream);
 int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream);
+/* fused layer tail (bf16 path): x' = x + o . Wo^T (o [M][256] bf16, skipped when o is NULL), then
+ * x = x' + W2 . GELU(W1 . LayerNorm(x')); plain [N][K] bf16 weights; cus picks the rows per workgroup */
+int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W1, const void* W2, const float* gamma,
+                   const float* beta, int cus, void* stream);
+/* the same with weights already packed (vap_test_pack_weight) */
+int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
+                          const float* gamma, const float* beta, int cus, void* stream);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
+/* timing diagnostics: 8 x 24 s_memtime stamps of sampled fused-block workgroups (VAP_BLOCK_STAMPS=1) */
+int vap_test_read_block_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 32 s_memtime stamps of sampled row-panel workgroups (VAP_RP_STAMPS=1) */
 int vap_test_read_rp_stamps(unsigned long long* out);
 /* timing diagnostics (VAP_FFN_STAMPS=1): 8 x 24 s_memtime stamps of sampled fused-FFN workgroups, then

@@ -274,3 +274,32 @@ def test_ffn_fused(M):
     ref = x + hdn @ W2.float().t()
     err = (dx.cpu() - ref).abs().max().item()
     assert err <= 2e-3 * max(1.0, ref.abs().max().item()), f"ffn M={M}: {err}"
+
+
+@pytest.mark.parametrize("M,cus", [(1, 256), (77, 256), (1000, 256), (1000, 8), (5000, 16), (4700, 256)])
+@pytest.mark.parametrize("oproj", [True, False])
+def test_block_fused(M, cus, oproj):
+    """Fused layer tail (k_block.hip): x' = x + O . Wo^T, x = x' + W2 . GELU(W1 . LN(x')), against the
+    torch fp32 composition on the same bf16-rounded operands (O and the weights bf16; the LN output
+    and the GELU output rounded to bf16 as the kernel does).  `cus` steers the rows per workgroup:
+    a small CU count forces the 144-row tiles."""
+    L = lib()
+    D = 256
+    g = torch.Generator().manual_seed(5 + M + cus)
+    x = torch.randn(M, D, generator=g) * 2 + 0.3
+    O = (torch.randn(M, D, generator=g)).to(torch.bfloat16)
+    ga = 1 + 0.2 * torch.randn(D, generator=g)
+    be = 0.1 * torch.randn(D, generator=g)
+    Wo = (torch.randn(D, D, generator=g) / 16).to(torch.bfloat16)
+    W1 = (torch.randn(3 * D, D, generator=g) / 16).to(torch.bfloat16)
+    W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16)
+    dx = x.clone().cuda()
+    dO, dWo = (O.cuda(), Wo.cuda()) if oproj else (None, None)
+    d = [t.cuda() for t in (W1, W2, ga, be)]
+    _run(L.lib().vap_test_block, _p(dx), _p(dO), M, _p(dWo), _p(d[0]), _p(d[1]), _p(d[2]), _p(d[3]), cus, _st())
+    xp = x + O.float() @ Wo.float().t() if oproj else x
+    a = F.layer_norm(xp, (D,), ga, be).to(torch.bfloat16).float()
+    hdn = F.gelu(a @ W1.float().t()).to(torch.bfloat16).float()
+    ref = xp + hdn @ W2.float().t()
+    err = (dx.cpu() - ref).abs().max().item()
+    assert err <= 2e-3 * max(1.0, ref.abs().max().item()), f"block M={M} cus={cus} oproj={oproj}: {err}"

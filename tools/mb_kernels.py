@@ -140,8 +140,22 @@ def bench_ffn(lib, dev, st, iters, M):
                                             1, 1, st))
         _native.check(lib.vap_test_gemm(1, ptr(FF), 3 * D, M * 3 * D, ptr(W2), 3 * D, D, None, M, 1, ptr(x), D, M * D,
                                         ptr(x), D, M * D, None, None, 0, 0, 1, st))
+    Wo = (torch.randn(D, D, generator=g) / 16).to(torch.bfloat16).to(dev)
+    Wop = torch.empty_like(Wo)
+    _native.check(lib.vap_test_pack_weight(ptr(Wo), ptr(Wop), D, D, st))
+    O = torch.randn(M, D, generator=g).to(torch.bfloat16).to(dev)
+    cus = int(os.environ.get("MB_CUS", "248"))
+
+    def block():  # out-proj + residual + LN + FFN + residual in one launch
+        _native.check(lib.vap_test_block_packed(ptr(x), ptr(O), M, ptr(Wop), ptr(W1p), ptr(W2p), ptr(ga), ptr(be),
+                                                cus, st))
+
+    def oproj_ffn():  # the pair it replaces: row-panel out-proj (+ residual) then the fused FFN
+        _native.check(lib.vap_test_rowpanel(ptr(O), D, M, ptr(Wop), D, D, ptr(x), D, ptr(x), None, None, 16, 2, st))
+        fused()
+
     res = {}
-    for name, fn in [("ffn_fused", fused), ("ffn_unfused", unfused)]:
+    for name, fn in [("ffn_fused", fused), ("ffn_unfused", unfused), ("oproj_ffn", oproj_ffn), ("block", block)]:
         us = timeit(fn, iters)
         res[name] = dict(us=round(us, 2), tflops=round(2.0 * M * 2 * 3 * D * D / us / 1e6, 1))
         print(name, res[name], flush=True)

@@ -1,0 +1,372 @@
+// Fused tail of a transformer layer (bf16 perf path):
+//
+//   x' = x + O . Wo^T                        attention output projection + residual (modules.py:96-110,
+//                                              :262 / :272, proj has no bias)
+//   x  = x' + W2 . GELU(W1 . LayerNorm(x'))  ffn_block + residual (modules.py:9-21, :274)
+//
+// One workgroup of 8 waves owns R = 16*MT rows (MT = 9: 144 rows, one workgroup per CU), so every
+// weight byte streamed from L2 feeds 144 rows instead of the 64 of the separate row-panel / FFN
+// kernels, and x' never goes to HBM (the unfused pair wrote x' and read it back: 2 x 33 MB per
+// 32k rows, one launch more).
+//
+// Wave w owns output columns 32w .. 32w+31 of EVERY row of the workgroup.  Its accumulators start
+// as the residual x, take the out-projection, then (after the LayerNorm) the three FFN-down
+// slices: acc[i][j] is the 16x16 C^T tile (output columns 32w + 16i .., rows 16j ..), a lane
+// holding 4 consecutive columns of one row (operands swapped: C^T = W . A^T).
+//   LayerNorm(x'): row sums of acc over the wave's 32 columns, cross-wave through LDS (two passes:
+//                  mean, then the centred variance), normalised rows -> bf16 panel P in LDS.
+//   FFN in 3 hidden slices of 256: up (K 256 from P) -> GELU -> bf16 slice H in LDS -> down
+//                  (K 256 of W2) accumulated into acc.  One barrier before H is overwritten, one
+//                  after it is written; waves drift freely inside each k-loop.
+// Weights come straight from L2 into registers in the packed row-panel layout (k_misc.hip
+// pack_rowpanel: fragment (k-step, 16-row group) = 1 KiB contiguous), NPF k-steps ahead, as one
+// stream over Wo (8 k-steps), then W1 slice s (8), W2 slice s (8) for s = 0..2.
+// LDS (MT = 9): P 72 KiB + H 72 KiB (the O panel at the start, then the hidden slices) + 2 x 4.5 KiB
+// row partials = 153 KiB.
+#include <cstdlib>
+
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+constexpr int D = 256;
+constexpr int ROWB = D * 2;  // bf16 row of the panel / of a hidden slice: 512 B = 32 chunks
+constexpr int NPF = 2;       // weight prefetch depth (k-steps)
+
+template <int MT> struct Blk {
+  static constexpr int R = 16 * MT;
+  static constexpr int OFF_H = R * ROWB;
+  static constexpr int OFF_RED = 2 * R * ROWB;  // [2][R][8] fp32 per-wave row partials
+  static constexpr int OFF_GB = OFF_RED + 2 * R * 8 * 4;  // LayerNorm gamma / beta
+  static constexpr int LDS = OFF_GB + 2 * D * 4;
+};
+
+// 16-B chunk c of row `row`: rows are 512 B (= 0 mod 256) apart, so XOR with row%16 spreads an
+// MFMA fragment read (16 rows, lane groups of ds_read_b128) over distinct bank groups
+VAP_DEV int xswz(int row, int c) { return c ^ (row & 15); }
+
+// GELU in sigmoid form, x * sigmoid(-x (c1 + c2 x^2) ln 2), with c1 / c2 fitted to the erf GELU
+// (max |error| 2.7e-4 over the reals, below half a bf16 ulp for |x| >= 0.14): one v_exp + one v_rcp
+// + 5 VALU.  Large negative x: exp2 -> +inf, rcp -> 0, result -0; large positive: x.
+VAP_DEV float gelu_sig(float x) {
+  const float u = x * __builtin_fmaf(x * x, -0.10012561f, -2.3087653f);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+}
+
+// diagnostics (VAP_BLOCK_STAMPS=1): wave 0 of workgroups 0, 32, .., 224 records s_memtime at [0] start,
+// [1] O panel in LDS, [2] out-projection done, [3] LayerNorm panel complete, per slice s [4+4s] up done,
+// [5+4s] GELU done + barrier, [6+4s] hidden slice written + barrier, [7+4s] down done, [16] stores
+// issued, [17] stores complete
+__device__ unsigned long long g_blk_stamps[8][24];
+
+template <int MT, bool OPROJ, bool ST = false>
+__global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
+  using C = Blk<MT>;
+  constexpr int R = C::R;
+  constexpr int Q0 = OPROJ ? 8 : 0;      // first FFN k-step of the weight stream
+  constexpr int NQ = Q0 + 48;            // Wo 8 + 3 x (W1 8 + W2 8)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+  unsigned char* P = smem;
+  unsigned char* H = smem + C::OFF_H;
+  float* red0 = (float*)(smem + C::OFF_RED);
+  float* red1 = red0 + R * 8;
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * R;
+  const int samp = (ST && (blockIdx.x & 31) == 0 && blockIdx.x < 256 && tid == 0) ? (int)(blockIdx.x >> 5) : -1;
+  // phase boundary (+ a stamp in the diagnostics build): the scheduling barrier also keeps the
+  // scheduler from mixing phases, which otherwise drives the 144-row variant into spills
+  unsigned long long stv[18];  // wave-uniform: SGPRs
+  auto stamp = [&](int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (g.M < 0) asm volatile("s_nop 0");  // never taken: splits the block (basic-block boundary)
+    if constexpr (ST) {
+      stv[k] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp(0);
+
+  auto roff = [&](int m, int64_t seq) -> int64_t {  // element offset of row m (256-wide rows)
+    if (g.rows_per_seq == 0) return (int64_t)m * D;
+    const int sq = m / g.rows_per_seq;
+    return (int64_t)sq * seq + (int64_t)(m - sq * g.rows_per_seq) * D;
+  };
+  // byte offsets (from row m0) of rows mf, mf + 16, .., mf + 16 (n - 1), 256-wide rows of esz-byte
+  // elements: one division, then stepping (rows >= M: out of range for the buffer resource)
+  auto rows16 = [&](int mf, int64_t seq, int64_t base, int esz, uint32_t* out, int n) {
+    int sq = 0, t = mf;
+    if (g.rows_per_seq) {
+      sq = mf / g.rows_per_seq;
+      t = mf - sq * g.rows_per_seq;
+    }
+    for (int k = 0; k < n; ++k) {
+      const int m = mf + 16 * k;
+      const int64_t e = g.rows_per_seq ? (int64_t)sq * seq + (int64_t)t * D : (int64_t)m * D;
+      out[k] = m < g.M ? (uint32_t)((e - base) * esz) : 0x80000000u;
+      t += 16;
+      if (g.rows_per_seq)
+        while (t >= g.rows_per_seq) {
+          t -= g.rows_per_seq;
+          ++sq;
+        }
+    }
+  };
+
+  // gamma / beta of the LayerNorm -> LDS (issued first: vmcnt counts in order)
+  float* GB = (float*)(smem + C::OFF_GB);
+  f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 128) gbv = *(const f32x4*)((tid < 64 ? g.gamma : g.beta) + (tid & 63) * 4);
+
+  // ---------------------------------------------------------------- O panel (bf16) and residual rows
+  // O first, so the out-projection waits for O only while x is still in flight; rows >= M read 0
+  constexpr int OPT = R * 32 / 512;  // O chunks per thread (R multiple of 16)
+  chunk16 ot[OPROJ ? OPT : 1];
+  if constexpr (OPROJ) {
+    const int64_t obase = roff(m0, g.o_seq);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(g.o + obase, 0x7FFFFFF0u);
+    uint32_t oo[OPT];
+    rows16(m0 + (tid >> 5), g.o_seq, obase, 2, oo, OPT);
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+  }
+  // lane's rows j*16 + l16 of x (recomputed for the stores at the end, not held live)
+  const int64_t xbase = roff(m0, g.x_seq);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
+  f32x4 acc[2][MT], xt[2][MT];
+  {
+    uint32_t xo[MT];
+    rows16(m0 + l16, g.x_seq, xbase, 4, xo, MT);
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
+        if constexpr (OPROJ) {
+          xt[i][j] = v;
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          acc[i][j] = v;
+        }
+      }
+  }
+
+  // ---------------------------------------------------------------- weight stream
+  const bf16* __restrict__ Wo = (const bf16*)g.Wo;
+  const bf16* __restrict__ W1 = (const bf16*)g.W1;
+  const bf16* __restrict__ W2 = (const bf16*)g.W2;
+  auto wload = [&](int q, chunk16* r) {  // q static after unrolling
+    const bf16* base;
+    int kidx;
+    if (OPROJ && q < Q0) {
+      base = Wo;
+      kidx = q;
+    } else {
+      const int t = q - Q0, s = t >> 4, u = t & 15;
+      base = u < 8 ? W1 : W2;
+      kidx = s * 8 + (u & 7);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+  };
+  chunk16 wr[NPF][2];
+#pragma unroll
+  for (int p = 0; p < NPF; ++p) wload(p, wr[p]);
+
+  // one k-step: acc[i][j] += W fragment i x A fragment j (A rows j*16 + l16 of an LDS image)
+  // fragment j of k-step ks sits at byte (j*16 + l16) * 512 + ((ks*4 + lg) ^ l16) * 16 = abase(j) ^ ks*64
+  // (ks*4 only touches chunk bits 2..4 and lg the low two, so the XOR splits)
+  const uint32_t afo = (uint32_t)(l16 * ROWB + (lg ^ l16) * 16);
+  auto kstep = [&](const unsigned char* img, int ks, int q, f32x4 (&c)[2][MT]) {
+    chunk16 af[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) af[j] = *(const chunk16*)(img + j * 16 * ROWB + (afo ^ (uint32_t)(ks * 64)));
+    chunk16* wf = wr[q % NPF];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) c[i][j] = mfma_chunk<bf16>(wf[i], af[j], c[i][j]);
+    // unconditional refill (the tail reloads the last step): a conditional load makes the
+    // compiler's vmcnt bookkeeping drain the whole prefetch
+    wload(q + NPF < NQ ? q + NPF : NQ - 1, wf);
+    // keep k-steps apart: left alone, the scheduler hoists later k-steps' fragment reads over
+    // earlier MFMAs and spills (the other wave on the SIMD covers the read latency instead)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if constexpr (OPROJ) {
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+      const int id = tid + k * 512, row = id >> 5, c = id & 31;
+      *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = ot[k];
+    }
+    if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
+    __syncthreads();
+    stamp(1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kstep(H, ks, ks, acc);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) acc[i][j] += xt[i][j];
+    stamp(2);
+  } else {
+    if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
+  }
+
+  // ---------------------------------------------------------------- LayerNorm(x') -> P
+  // row partials over the wave's 32 columns: sum over the 4 lane groups with permlane swaps (VALU,
+  // no LDS round trip), then one LDS word per (row, wave); every lane group writes the same value
+  {
+#ifdef VAP_BLOCK_SHFL
+    auto gsum = [](float v) {
+      v += __shfl_xor(v, 16, 64);
+      return v + __shfl_xor(v, 32, 64);
+    };
+#else
+    auto gsum = [](float v) {  // sum over the 4 16-lane groups
+      // inline asm: the builtins on two copies of one value were folded to a + a (ROCm 7.2 clang);
+      // the s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see
+      float a = v, b = v;
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+      float c = a + b, d = c;
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+      return c + d;
+    };
+#endif
+    auto rowtot = [&](const float* red, int j) {
+      const f32x4 a = *(const f32x4*)(red + (j * 16 + l16) * 8), b = *(const f32x4*)(red + (j * 16 + l16) * 8 + 4);
+      return ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+    };
+    float mean[MT], rstd[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+      red0[(j * 16 + l16) * 8 + w] = gsum(s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      mean[j] = rowtot(red0, j) * (1.0f / D);
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[i][j][e] - mean[j];
+          s += d * d;
+        }
+      red1[(j * 16 + l16) * 8 + w] = gsum(s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT; ++j) rstd[j] = rsqrtf(rowtot(red1, j) * (1.0f / D) + g.eps);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = w * 32 + i * 16 + lg * 4;
+      const f32x4 ga = *(const f32x4*)(GB + n), be = *(const f32x4*)(GB + 256 + n);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int row = j * 16 + l16;
+        const f32x4 y = (acc[i][j] - mean[j]) * rstd[j] * ga + be;
+        *(u32x2*)(P + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = pack_bf16x4(y[0], y[1], y[2], y[3]);
+      }
+    }
+  }
+  __syncthreads();  // P complete
+  stamp(3);
+
+  // ---------------------------------------------------------------- FFN, 3 hidden slices of 256
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    f32x4 up[2][MT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) up[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kstep(P, ks, Q0 + 16 * s + ks, up);
+    stamp(4 + 4 * s);
+    u32x2 hb[2][MT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+        hb[i][j] = pack_bf16x4(gelu_sig(up[i][j][0]), gelu_sig(up[i][j][1]), gelu_sig(up[i][j][2]),
+                               gelu_sig(up[i][j][3]));
+    __syncthreads();  // every wave is done reading H (the O panel / the previous slice)
+    stamp(5 + 4 * s);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = w * 32 + i * 16 + lg * 4;
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int row = j * 16 + l16;
+        *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = hb[i][j];
+      }
+    }
+    __syncthreads();  // slice s of the hidden complete
+    stamp(6 + 4 * s);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kstep(H, ks, Q0 + 16 * s + 8 + ks, acc);
+    stamp(7 + 4 * s);
+  }
+
+  // ---------------------------------------------------------------- x = acc (fp32, in place)
+  int z;  // opaque zero: the offsets are recomputed here rather than kept live from the prologue
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  {
+    uint32_t xo[MT];
+    rows16(m0 + l16 + z, g.x_seq, xbase, 4, xo, MT);
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+  }
+  if constexpr (ST) {
+    stamp(16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(17);
+    if (samp >= 0)
+      for (int k = 0; k < 18; ++k) g_blk_stamps[samp][k] = stv[k];
+  }
+}
+
+template <int MT>
+hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
+  const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
+  static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
+  if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
+  else if (g.o) hipLaunchKernelGGL((block_kernel<MT, true>), grid, dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((block_kernel<MT, false>), grid, dim3(512), 0, st, g);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// rows per workgroup: 64 (MT 4: 70 KiB LDS and 126 VGPRs, so two workgroups share a CU and one's
+// HBM phases overlap the other's matrix work: 40 us per 32k rows) unless VAP_BLOCK_MT=9 (144 rows,
+// one workgroup per CU, weights streamed once per 144 rows: 47 us, its HBM load / store phases
+// exposed); `cus` = 0 selects the default, a positive count lets MT 9 take inputs that 2 x cus
+// 64-row workgroups would not cover in one round
+hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st) {
+  if (g.M <= 0 || g.rows_per_seq < 0 || !g.x || !g.W1 || !g.W2 || (g.o && !g.Wo)) return hipErrorInvalidValue;
+  static const int force = getenv("VAP_BLOCK_MT") ? atoi(getenv("VAP_BLOCK_MT")) : 0;
+  const int mt = force ? force : (cus > 0 && cus < 64 && (g.M + 63) / 64 > 2 * cus ? 9 : 4);
+  const int bm = 16 * mt;
+  // a panel's rows must lie within the 2 GiB a buffer offset reaches from its first row
+  const int64_t span = g.rows_per_seq ? (bm / g.rows_per_seq + 2) * g.x_seq + (int64_t)bm * D : (int64_t)bm * D;
+  if (span * 4 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+  if (mt == 4) return launch_mt<4>(g, st);
+  if (mt == 9) return launch_mt<9>(g, st);
+  return hipErrorInvalidValue;
+}
+
+// diagnostics: copy the block-kernel phase stamps (8 sampled workgroups x 24) to host memory
+hipError_t read_block_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_stamps), sizeof(g_blk_stamps), 0, hipMemcpyDeviceToHost);
+}

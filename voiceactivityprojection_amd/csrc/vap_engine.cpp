@@ -54,6 +54,8 @@ struct vap_handle {
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
   bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
+  bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
+                            // (k_block.hip); VAP_BLOCK=0 selects the separate row-panel + FFN kernels
   bool ffn_fused = true;  // bf16 FFN with the hidden in LDS (k_ffn.hip): 62 us vs 93 us for the unfused
                           // row-panel up + GEMM down per 32k rows; VAP_FFN_FUSED=0 selects the unfused pair
   hipStream_t side[NSIDE] = {};
@@ -560,7 +562,9 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     HIPCHK(launch_attention<T>(a, st));
     if (int rc = attn_maps<T>(h, a, cross ? 2 : 0, layer, r, st)) return rc;
   }
-  {
+  // the layer's last out-projection goes into the fused block kernel with the FFN
+  const bool blk = h->block_fused && h->ffn_fused;
+  if (cross || !blk) {
     Timed tm(h, VAP_K_TR_GEMM, st);
     HIPCHK(rp(ATT, D, pre + ".o", D, X, D, X, "", 0, 2));
   }
@@ -576,14 +580,18 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       HIPCHK(launch_attention<T>(a, st));
       if (int rc = attn_maps<T>(h, a, 1, layer, r, st)) return rc;
     }
-    {
+    if (!blk) {
       Timed tm(h, VAP_K_TR_GEMM, st);
       HIPCHK(rp(ATT, D, pre + ".oc", D, X, D, X, "", 0, 2));
     }
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    if (h->ffn_fused) {
+    if (blk) {
+      BlockArgs b{X, ATT, rows, 0, 0, 0, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")), h->W<T>(pre + ".w1@rp"),
+                  h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"), h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+      HIPCHK(launch_block(b, 0, st));
+    } else if (h->ffn_fused) {
       FfnArgs f{X, rows, 0, 0, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
       HIPCHK(launch_ffn(f, st));
@@ -894,7 +902,8 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     a.q0 = f0;
     HIPCHK(launch_attention<T>(a, st));
   }
-  {
+  const bool blk = h->block_fused && h->ffn_fused;  // last out-projection fused with the FFN
+  if (cross || !blk) {
     Timed tm(h, VAP_K_TR_GEMM, st);
     HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".o", D, Xf, D, t1, Xf, "", 0, 2));
   }
@@ -910,14 +919,19 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       a.q0 = f0;
       HIPCHK(launch_attention<T>(a, st));
     }
-    {
+    if (!blk) {
       Timed tm(h, VAP_K_TR_GEMM, st);
       HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".oc", D, Xf, D, t1, Xf, "", 0, 2));
     }
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
+    if (blk) {  // out-proj + residual + LN + FFN + residual (k_block.hip)
+      BlockArgs b{Xf, ATT + (int64_t)f0 * D, S * nf, nf, t1, t1, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")),
+                  h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
+                  h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+      HIPCHK(launch_block(b, 0, st));
+    } else if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
       FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
       HIPCHK(launch_ffn(f, st));
@@ -1490,6 +1504,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
   if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
   if (const char* e = getenv("VAP_FFN_FUSED")) h->ffn_fused = atoi(e) != 0;
+  if (const char* e = getenv("VAP_BLOCK")) h->block_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);

@@ -177,3 +177,21 @@ struct FfnArgs {
   float eps;
 };
 hipError_t launch_ffn(const FfnArgs& g, hipStream_t st);
+// Fused layer tail (k_block.hip): x' = x + o . Wo^T (skipped when o is null), then
+// x = x' + W2 . GELU(W1 . LayerNorm(x')); weights in the packed row-panel layout.
+struct BlockArgs {
+  float* x;           // residual rows, fp32, in / out
+  const bf16* o;      // attention output rows (bf16) or nullptr
+  int M;
+  int rows_per_seq;   // 0: rows contiguous (stride 256)
+  int64_t x_seq;      // sequence strides (elements) of x / o when rows_per_seq > 0
+  int64_t o_seq;
+  const void* Wo;
+  const void* W1;
+  const void* W2;
+  const float* gamma;
+  const float* beta;
+  float eps;
+};
+hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st);
+hipError_t read_block_stamps(unsigned long long* out);

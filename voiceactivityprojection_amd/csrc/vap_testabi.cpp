@@ -147,6 +147,29 @@ int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* g
 }
 
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
+// fused layer tail: x = x' + FFN(LN(x')), x' = x + o . Wo^T (o may be null); plain [N][K] weights
+int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W1, const void* W2, const float* gamma,
+                   const float* beta, int cus, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  void* p = nullptr;
+  const size_t n1 = 768 * 256, n0 = 256 * 256;
+  if (hipMalloc(&p, (2 * n1 + n0) * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+  bf16 *p1 = (bf16*)p, *p2 = p1 + n1, *p0 = p2 + n1;
+  hipError_t e = launch_pack_rowpanel((const bf16*)W1, p1, 768, 256, st);
+  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)W2, p2, 256, 768, st);
+  if (e == hipSuccess && Wo) e = launch_pack_rowpanel((const bf16*)Wo, p0, 256, 256, st);
+  BlockArgs g{x, (const bf16*)o, M, 0, 0, 0, Wo ? p0 : nullptr, p1, p2, gamma, beta, 1e-5f};
+  if (e == hipSuccess) e = launch_block(g, cus, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(p);
+  return rc_of(e);
+}
+int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
+                          const float* gamma, const float* beta, int cus, void* stream) {
+  BlockArgs g{x, (const bf16*)o, M, 0, 0, 0, Wop, W1p, W2p, gamma, beta, 1e-5f};
+  return rc_of(launch_block(g, cus, (hipStream_t)stream));
+}
+int vap_test_read_block_stamps(unsigned long long* out) { return rc_of(read_block_stamps(out)); }
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
 int vap_test_read_gemm_stamps(unsigned long long* out) { return rc_of(read_gemm2_stamps(out)); }
