@@ -197,6 +197,11 @@ int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* g
  * x = x' + W2 . GELU(W1 . LayerNorm(x')); plain [N][K] bf16 weights; cus picks the rows per workgroup */
 int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W1, const void* W2, const float* gamma,
                    const float* beta, int cus, void* stream);
+/* fused LayerNorm'd projections (bf16 path), plain [N][256] bf16 weights: with o (np = 1):
+ * x' = x + o . Wo^T is stored to x and cp [M][256] = LN(x') . Wp^T; without o (np = 3):
+ * cp [M][768] = LN(x) . Wp^T and, nr = 2, cr [M][512] = x . Wr^T from the raw rows */
+int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* Wp, int np, const void* Wr, int nr,
+                    void* cp, void* cr, const float* gamma, const float* beta, void* stream);
 /* the same with weights already packed (vap_test_pack_weight) */
 int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
                           const float* gamma, const float* beta, int cus, void* stream);

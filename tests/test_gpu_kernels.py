@@ -303,3 +303,39 @@ def test_block_fused(M, cus, oproj):
     ref = xp + hdn @ W2.float().t()
     err = (dx.cpu() - ref).abs().max().item()
     assert err <= 2e-3 * max(1.0, ref.abs().max().item()), f"block M={M} cus={cus} oproj={oproj}: {err}"
+
+
+@pytest.mark.parametrize("M", [1, 77, 1000, 4700])
+@pytest.mark.parametrize("mode", ["oproj_qc", "qkv", "qkv_kvc"])
+def test_lnproj_fused(M, mode):
+    """Fused LayerNorm'd projections (k_block.hip lnproj): oproj_qc = x' = x + O . Wo^T (stored) and
+    LN(x') . Wqc^T; qkv = LN(x) . Wqkv^T; qkv_kvc = that plus the raw-row cross K/V x . Wkv^T, against
+    the torch fp32 composition on the same bf16-rounded operands (bf16 outputs)."""
+    L = lib()
+    D = 256
+    g = torch.Generator().manual_seed(11 + M)
+    x = torch.randn(M, D, generator=g) * 2 + 0.3
+    O = torch.randn(M, D, generator=g).to(torch.bfloat16)
+    ga = 1 + 0.2 * torch.randn(D, generator=g)
+    be = 0.1 * torch.randn(D, generator=g)
+    oproj = mode == "oproj_qc"
+    np_, nr = (1, 0) if oproj else (3, 2 if mode == "qkv_kvc" else 0)
+    Wo = (torch.randn(D, D, generator=g) / 16).to(torch.bfloat16)
+    Wp = (torch.randn(np_ * D, D, generator=g) / 16).to(torch.bfloat16)
+    Wr = (torch.randn(max(nr, 1) * D, D, generator=g) / 16).to(torch.bfloat16)
+    dx = x.clone().cuda()
+    cp = torch.zeros(M, np_ * D, dtype=torch.bfloat16, device="cuda")
+    cr = torch.zeros(M, max(nr, 1) * D, dtype=torch.bfloat16, device="cuda")
+    d = [t.cuda() for t in (O, Wo, Wp, Wr, ga, be)]
+    _run(L.lib().vap_test_lnproj, _p(dx), _p(d[0]) if oproj else None, M, _p(d[1]) if oproj else None, _p(d[2]),
+         np_, _p(d[3]) if nr else None, nr, _p(cp), _p(cr) if nr else None, _p(d[4]), _p(d[5]), _st())
+    xp = x + O.float() @ Wo.float().t() if oproj else x
+    assert (dx.cpu() - xp).abs().max().item() <= 1e-4 * max(1.0, xp.abs().max().item()), "x'"
+    a = F.layer_norm(xp, (D,), ga, be).to(torch.bfloat16).float()
+    ref = a @ Wp.float().t()
+    err = (cp.float().cpu() - ref).abs().max().item()
+    assert err <= 1e-2 * max(1.0, ref.abs().max().item()), f"cp {mode} M={M}: {err}"
+    if nr:
+        refr = x.to(torch.bfloat16).float() @ Wr.float().t()
+        errr = (cr.float().cpu() - refr).abs().max().item()
+        assert errr <= 1e-2 * max(1.0, refr.abs().max().item()), f"cr M={M}: {errr}"

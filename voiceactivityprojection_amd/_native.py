@@ -81,6 +81,7 @@ _SIGS = {
     "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_ffn_packed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_block": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_int, _P]),
+    "vap_test_lnproj": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_block_packed": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "vap_test_rowpanel": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _I64,
                                          _P, _P, _P, ctypes.c_int, ctypes.c_int, _P]),

@@ -54,6 +54,90 @@ VAP_DEV float gelu_sig(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
 }
 
+// Byte offsets (from element `base`) of rows mf, mf + 16, .., mf + 16 (n - 1) of a row set whose
+// row m sits at element (m / rps) * seq + (m % rps) * ld (rps = 0: m * ld), esz-byte elements: one
+// division, then stepping.  Rows >= M get an offset outside every buffer resource (reads 0, stores
+// drop).
+VAP_DEV void rows16_off(int mf, int M, int rps, int64_t seq, int64_t ld, int64_t base, int esz, uint32_t* out, int n) {
+  int sq = 0, t = mf;
+  if (rps) {
+    sq = mf / rps;
+    t = mf - sq * rps;
+  }
+  for (int k = 0; k < n; ++k) {
+    const int m = mf + 16 * k;
+    const int64_t e = rps ? (int64_t)sq * seq + (int64_t)t * ld : (int64_t)m * ld;
+    out[k] = m < M ? (uint32_t)((e - base) * esz) : 0x80000000u;
+    t += 16;
+    if (rps)
+      while (t >= rps) {
+        t -= rps;
+        ++sq;
+      }
+  }
+}
+
+// LayerNorm of the R rows held in acc (wave w: columns 32w .. 32w+31; lane: row j*16 + l16, columns
+// 32w + 16i + 4lg ..) -> bf16 panel P (XOR-swizzled rows), gamma / beta from GB[0..255] / GB[256..511].
+// Row partials over the wave's 32 columns are summed over the 4 lane groups with permlane swaps
+// (VALU, no LDS round trip), then exchanged as one LDS word per (row, wave): two passes (mean, then
+// the centred variance), two barriers.  The caller's barrier publishes P.
+template <int MT>
+VAP_DEV void ln_panel(const f32x4 (&acc)[2][MT], float* red0, float* red1, const float* GB, unsigned char* P, int w,
+                      int l16, int lg, float eps) {
+  {  // every lane group writes the same partial
+    auto gsum = [](float v) {  // sum over the 4 16-lane groups
+      // inline asm: the builtins on two copies of one value were folded to a + a (ROCm 7.2 clang);
+      // the s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see
+      float a = v, b = v;
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+      float c = a + b, d = c;
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+      return c + d;
+    };
+    auto rowtot = [&](const float* red, int j) {
+      const f32x4 a = *(const f32x4*)(red + (j * 16 + l16) * 8), b = *(const f32x4*)(red + (j * 16 + l16) * 8 + 4);
+      return ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+    };
+    float mean[MT], rstd[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+      red0[(j * 16 + l16) * 8 + w] = gsum(s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      mean[j] = rowtot(red0, j) * (1.0f / D);
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[i][j][e] - mean[j];
+          s += d * d;
+        }
+      red1[(j * 16 + l16) * 8 + w] = gsum(s);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT; ++j) rstd[j] = rsqrtf(rowtot(red1, j) * (1.0f / D) + eps);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = w * 32 + i * 16 + lg * 4;
+      const f32x4 ga = *(const f32x4*)(GB + n), be = *(const f32x4*)(GB + 256 + n);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int row = j * 16 + l16;
+        const f32x4 y = (acc[i][j] - mean[j]) * rstd[j] * ga + be;
+        *(u32x2*)(P + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = pack_bf16x4(y[0], y[1], y[2], y[3]);
+      }
+    }
+  }
+}
+
 // diagnostics (VAP_BLOCK_STAMPS=1): wave 0 of workgroups 0, 32, .., 224 records s_memtime at [0] start,
 // [1] O panel in LDS, [2] out-projection done, [3] LayerNorm panel complete, per slice s [4+4s] up done,
 // [5+4s] GELU done + barrier, [6+4s] hidden slice written + barrier, [7+4s] down done, [16] stores
@@ -93,25 +177,8 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     const int sq = m / g.rows_per_seq;
     return (int64_t)sq * seq + (int64_t)(m - sq * g.rows_per_seq) * D;
   };
-  // byte offsets (from row m0) of rows mf, mf + 16, .., mf + 16 (n - 1), 256-wide rows of esz-byte
-  // elements: one division, then stepping (rows >= M: out of range for the buffer resource)
   auto rows16 = [&](int mf, int64_t seq, int64_t base, int esz, uint32_t* out, int n) {
-    int sq = 0, t = mf;
-    if (g.rows_per_seq) {
-      sq = mf / g.rows_per_seq;
-      t = mf - sq * g.rows_per_seq;
-    }
-    for (int k = 0; k < n; ++k) {
-      const int m = mf + 16 * k;
-      const int64_t e = g.rows_per_seq ? (int64_t)sq * seq + (int64_t)t * D : (int64_t)m * D;
-      out[k] = m < g.M ? (uint32_t)((e - base) * esz) : 0x80000000u;
-      t += 16;
-      if (g.rows_per_seq)
-        while (t >= g.rows_per_seq) {
-          t -= g.rows_per_seq;
-          ++sq;
-        }
-    }
+    rows16_off(mf, g.M, g.rows_per_seq, seq, D, base, esz, out, n);
   };
 
   // gamma / beta of the LayerNorm -> LDS (issued first: vmcnt counts in order)
@@ -216,66 +283,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   }
 
   // ---------------------------------------------------------------- LayerNorm(x') -> P
-  // row partials over the wave's 32 columns: sum over the 4 lane groups with permlane swaps (VALU,
-  // no LDS round trip), then one LDS word per (row, wave); every lane group writes the same value
-  {
-#ifdef VAP_BLOCK_SHFL
-    auto gsum = [](float v) {
-      v += __shfl_xor(v, 16, 64);
-      return v + __shfl_xor(v, 32, 64);
-    };
-#else
-    auto gsum = [](float v) {  // sum over the 4 16-lane groups
-      // inline asm: the builtins on two copies of one value were folded to a + a (ROCm 7.2 clang);
-      // the s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see
-      float a = v, b = v;
-      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-      float c = a + b, d = c;
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
-      return c + d;
-    };
-#endif
-    auto rowtot = [&](const float* red, int j) {
-      const f32x4 a = *(const f32x4*)(red + (j * 16 + l16) * 8), b = *(const f32x4*)(red + (j * 16 + l16) * 8 + 4);
-      return ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
-    };
-    float mean[MT], rstd[MT];
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
-      red0[(j * 16 + l16) * 8 + w] = gsum(s);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      mean[j] = rowtot(red0, j) * (1.0f / D);
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = acc[i][j][e] - mean[j];
-          s += d * d;
-        }
-      red1[(j * 16 + l16) * 8 + w] = gsum(s);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < MT; ++j) rstd[j] = rsqrtf(rowtot(red1, j) * (1.0f / D) + g.eps);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = w * 32 + i * 16 + lg * 4;
-      const f32x4 ga = *(const f32x4*)(GB + n), be = *(const f32x4*)(GB + 256 + n);
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int row = j * 16 + l16;
-        const f32x4 y = (acc[i][j] - mean[j]) * rstd[j] * ga + be;
-        *(u32x2*)(P + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = pack_bf16x4(y[0], y[1], y[2], y[3]);
-      }
-    }
-  }
+  ln_panel<MT>(acc, red0, red1, GB, P, w, l16, lg, g.eps);
   __syncthreads();  // P complete
   stamp(3);
 
@@ -369,4 +377,196 @@ hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st) {
 // diagnostics: copy the block-kernel phase stamps (8 sampled workgroups x 24) to host memory
 hipError_t read_block_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_stamps), sizeof(g_blk_stamps), 0, hipMemcpyDeviceToHost);
+}
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm'd projections of a transformer layer in one launch (bf16 perf path), the same row-block
+// structure as block_kernel (8 waves, wave w owns columns 32w .. 32w+31 of every 256-wide output
+// tile, R = 16*MT rows, weights straight from L2):
+//   OPROJ:  x' = x + O . Wo^T stored back to x (fp32) and kept in registers; C_p = LN(x') . Wp^T
+//           -- the stereo layer's self-attention out-projection + LN_src + cross Q (modules.py:262-269)
+//   !OPROJ: C_p = LN(x) . Wp^T (QKV) and, NR > 0, C_r = x . Wr^T from the raw rows (the cross K/V of
+//           modules.py:265-272 take the UN-normalised pre-layer x): x is read from HBM once.
+// NP / NR = 256-wide N tiles of C_p / C_r.  bf16 outputs leave as 16-B stores: v_permlane16_swap
+// trades the two 16-column blocks between lane groups so a lane holds 8 consecutive columns.
+namespace {
+
+template <int MT, bool OPROJ, int NP, int NR>
+__global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs g) {
+  static_assert(!(OPROJ && NR), "the raw panel shares H with the O panel");
+  using C = Blk<MT>;
+  constexpr int R = C::R;
+  constexpr int Q0 = OPROJ ? 8 : 0;
+  constexpr int NQ = Q0 + 8 * (NP + NR);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+  unsigned char* P = smem;
+  unsigned char* H = smem + C::OFF_H;
+  float* red0 = (float*)(smem + C::OFF_RED);
+  float* red1 = red0 + R * 8;
+  float* GB = (float*)(smem + C::OFF_GB);
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * R;
+  const int rps = g.rows_per_seq;
+  auto roff = [&](int m, int64_t seq, int64_t ld) -> int64_t {
+    if (rps == 0) return (int64_t)m * ld;
+    const int sq = m / rps;
+    return (int64_t)sq * seq + (int64_t)(m - sq * rps) * ld;
+  };
+
+  f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 128) gbv = *(const f32x4*)((tid < 64 ? g.gamma : g.beta) + (tid & 63) * 4);
+
+  constexpr int OPT = R * 32 / 512;
+  chunk16 ot[OPROJ ? OPT : 1];
+  if constexpr (OPROJ) {
+    const int64_t obase = roff(m0, g.o_seq, D);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(g.o + obase, 0x7FFFFFF0u);
+    uint32_t oo[OPT];
+    rows16_off(m0 + (tid >> 5), g.M, rps, g.o_seq, D, obase, 2, oo, OPT);
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+  }
+  const int64_t xbase = roff(m0, g.x_seq, D);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
+  uint32_t xo[MT];
+  rows16_off(m0 + l16, g.M, rps, g.x_seq, D, xbase, 4, xo, MT);
+  // accumulators start as x (OPROJ: the out-projection adds onto them; x is issued after O, so the
+  // O panel can land while x is in flight)
+  f32x4 acc[2][MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      acc[i][j] = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
+
+  const bf16* __restrict__ Wo = (const bf16*)g.Wo;
+  const bf16* __restrict__ Wp = (const bf16*)g.Wp;
+  const bf16* __restrict__ Wr = (const bf16*)g.Wr;
+  auto wload = [&](int q, chunk16* r) {
+    const bf16* base;
+    int kidx;
+    if (OPROJ && q < Q0) {
+      base = Wo;
+      kidx = q;
+    } else {
+      const int p = (q - Q0) >> 3;
+      base = p < NP ? Wp : Wr;
+      kidx = (p < NP ? p : p - NP) * 8 + ((q - Q0) & 7);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+  };
+  chunk16 wr[NPF][2];
+#pragma unroll
+  for (int p = 0; p < NPF; ++p) wload(p, wr[p]);
+  const uint32_t afo = (uint32_t)(l16 * ROWB + (lg ^ l16) * 16);
+  auto kstep = [&](const unsigned char* img, int ks, int q, f32x4 (&c)[2][MT]) {
+    chunk16 af[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) af[j] = *(const chunk16*)(img + j * 16 * ROWB + (afo ^ (uint32_t)(ks * 64)));
+    chunk16* wf = wr[q % NPF];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) c[i][j] = mfma_chunk<bf16>(wf[i], af[j], c[i][j]);
+    wload(q + NPF < NQ ? q + NPF : NQ - 1, wf);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
+  if constexpr (OPROJ) {
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+      const int id = tid + k * 512, row = id >> 5, c = id & 31;
+      *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = ot[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kstep(H, ks, ks, acc);
+    // x' back to HBM now (it is the residual the cross attention adds to)
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+  }
+  if constexpr (NR > 0) {  // raw rows (bf16) -> H
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = w * 32 + i * 16 + lg * 4;
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int row = j * 16 + l16;
+        *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
+            pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  ln_panel<MT>(acc, red0, red1, GB, P, w, l16, lg, g.eps);
+  __syncthreads();  // P (and the raw panel) complete
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---------------------------------------------------------------- projections, one N tile per pass
+#pragma unroll
+  for (int p = 0; p < NP + NR; ++p) {
+    const bool raw = p >= NP;
+    const int nt = raw ? p - NP : p;
+    f32x4 c[2][MT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) c[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) kstep(raw ? H : P, ks, Q0 + 8 * p + ks, c);
+    bf16* out = raw ? g.cr : g.cp;
+    const int64_t ld = raw ? g.ldr : g.ldp, seq = raw ? g.cr_seq : g.cp_seq;
+    const int64_t cbase = roff(m0, seq, ld);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(out + cbase, 0x7FFFFFF0u);
+    uint32_t co[MT];
+    rows16_off(m0 + l16, g.M, rps, seq, ld, cbase, 2, co, MT);
+    const uint32_t col = (uint32_t)(nt * 256 + w * 32 + (lg & 1) * 16 + (lg >> 1) * 8);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      u32x2 a = pack_bf16x4(c[0][j][0], c[0][j][1], c[0][j][2], c[0][j][3]);
+      u32x2 b = pack_bf16x4(c[1][j][0], c[1][j][1], c[1][j][2], c[1][j][3]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(a[d], b[d], false, false);
+        a[d] = sw[0];
+        b[d] = sw[1];
+      }
+      buf_store16(rc, co[j] + col * 2u, u32x4{a[0], a[1], b[0], b[1]});
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int MT>
+hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
+  const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
+  if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0>), grid, dim3(512), 0, st, g);
+  else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0>), grid, dim3(512), 0, st, g);
+  else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2>), grid, dim3(512), 0, st, g);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// supported: (o, np 1, nr 0) out-proj + LN + cross Q; (no o, np 3, nr 0) LN + QKV; (no o, np 3, nr 2)
+// LN + QKV and raw cross K/V.  64-row workgroups (two per CU)
+hipError_t launch_lnproj(const LnProjArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.rows_per_seq < 0 || !g.x || !g.Wp || !g.cp || (g.o && !g.Wo) || (g.nr && (!g.Wr || !g.cr)))
+    return hipErrorInvalidValue;
+  constexpr int bm = 64;
+  // a workgroup's rows must lie within the 2 GiB a buffer offset reaches from its first row
+  auto span = [&](int64_t seq, int64_t ld, int esz) {
+    return (g.rows_per_seq ? (bm / g.rows_per_seq + 2) * seq + (int64_t)bm * ld : (int64_t)bm * ld) * esz;
+  };
+  if (span(g.x_seq, D, 4) >= 0x7FFFFFF0LL || span(g.cp_seq, g.ldp, 2) >= 0x7FFFFFF0LL ||
+      (g.nr && span(g.cr_seq, g.ldr, 2) >= 0x7FFFFFF0LL) || (g.o && span(g.o_seq, D, 2) >= 0x7FFFFFF0LL))
+    return hipErrorInvalidValue;
+  return launch_lnproj_mt<4>(g, st);
 }

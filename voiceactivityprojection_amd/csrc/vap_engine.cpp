@@ -54,6 +54,8 @@ struct vap_handle {
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
   bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
+  bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
+                             // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
   bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
                             // (k_block.hip); VAP_BLOCK=0 selects the separate row-panel + FFN kernels
   bool ffn_fused = true;  // bf16 FFN with the hidden in LDS (k_ffn.hip): 62 us vs 93 us for the unfused
@@ -889,11 +891,27 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     return launch_rowpanel(a, amode, epi, st);
   };
   float* Xf = X + (int64_t)f0 * D;
+  // fused LN projections (k_block.hip): rows (s, t in [f0, f1)), x / o / outputs at row f0 of sequence 0
+  auto lnp = [&](const T* o, const std::string& wo, const std::string& wp, int np, T* cp, int64_t ldp, int64_t cpseq,
+                 const std::string& wr, int nr, T* cr, int64_t ldr, int64_t crseq, const std::string& ln) {
+    LnProjArgs a{};
+    a.x = Xf; a.o = o; a.M = S * nf; a.rows_per_seq = nf; a.x_seq = t1; a.o_seq = t1;
+    a.Wo = o ? h->W<T>(wo + "@rp") : nullptr; a.Wp = h->W<T>(wp + "@rp"); a.Wr = nr ? h->W<T>(wr + "@rp") : nullptr;
+    a.cp = cp; a.ldp = ldp; a.cp_seq = cpseq; a.cr = cr; a.ldr = ldr; a.cr_seq = crseq;
+    a.gamma = h->P(ln + ".weight"); a.beta = h->P(ln + ".bias"); a.eps = 1e-5f; a.np = np; a.nr = nr;
+    return launch_lnproj(a, st);
+  };
+  const bool lnpf = h->lnproj_fused;
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(Xf, D, t1, pre + ".qkv", 3 * D, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_self_attn", 1, 0));
-    if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
-      HIPCHK(rp(Xf, D, t1, pre + ".kvc", 2 * D, KVC + (int64_t)f0 * 2 * D, 2 * D, t2, nullptr, "", 2, 0));
+    if (lnpf) {  // LN + QKV and the raw-row cross K/V from one read of x
+      HIPCHK(lnp(nullptr, "", pre + ".qkv", 3, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, pre + ".kvc", cross ? 2 : 0,
+                 KVC + (int64_t)f0 * 2 * D, 2 * D, t2, pre + ".ln_self_attn"));
+    } else {
+      HIPCHK(rp(Xf, D, t1, pre + ".qkv", 3 * D, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_self_attn", 1, 0));
+      if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
+        HIPCHK(rp(Xf, D, t1, pre + ".kvc", 2 * D, KVC + (int64_t)f0 * 2 * D, 2 * D, t2, nullptr, "", 2, 0));
+    }
   }
   {
     Timed tm(h, VAP_K_ATTN, st);
@@ -903,12 +921,16 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     HIPCHK(launch_attention<T>(a, st));
   }
   const bool blk = h->block_fused && h->ffn_fused;  // last out-projection fused with the FFN
-  if (cross || !blk) {
+  if (cross && lnpf) {  // out-proj + residual + LN_src + cross Q
+    Timed tm(h, VAP_K_TR_GEMM, st);
+    HIPCHK(lnp(ATT + (int64_t)f0 * D, pre + ".o", pre + ".qc", 1, QC + (int64_t)f0 * D, D, t1, "", 0, nullptr, 0, 0,
+               pre + ".ln_src_attn"));
+  } else if (cross || !blk) {
     Timed tm(h, VAP_K_TR_GEMM, st);
     HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".o", D, Xf, D, t1, Xf, "", 0, 2));
   }
   if (cross) {
-    {
+    if (!lnpf) {
       Timed tm(h, VAP_K_TR_GEMM, st);
       HIPCHK(rp(Xf, D, t1, pre + ".qc", D, QC + (int64_t)f0 * D, D, t1, nullptr, pre + ".ln_src_attn", 1, 0));
     }
@@ -1505,6 +1527,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
   if (const char* e = getenv("VAP_FFN_FUSED")) h->ffn_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_BLOCK")) h->block_fused = atoi(e) != 0;
+  if (const char* e = getenv("VAP_LNPROJ")) h->lnproj_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);

@@ -195,3 +195,25 @@ struct BlockArgs {
 };
 hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);
+// LayerNorm'd projections of a layer in one launch (k_block.hip): with o, x' = x + o . Wo^T is stored
+// to x and cp = LN(x') . Wp^T; without, cp = LN(x) . Wp^T and (nr > 0) cr = x . Wr^T from the raw
+// rows.  np / nr = 256-wide N tiles; packed row-panel weights; bf16 outputs.
+struct LnProjArgs {
+  float* x;
+  const bf16* o;
+  int M;
+  int rows_per_seq;
+  int64_t x_seq, o_seq;
+  const void* Wo;
+  const void* Wp;
+  const void* Wr;
+  bf16* cp;
+  int64_t ldp, cp_seq;
+  bf16* cr;
+  int64_t ldr, cr_seq;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  int np, nr;
+};
+hipError_t launch_lnproj(const LnProjArgs& g, hipStream_t st);

@@ -169,6 +169,28 @@ int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const
   BlockArgs g{x, (const bf16*)o, M, 0, 0, 0, Wop, W1p, W2p, gamma, beta, 1e-5f};
   return rc_of(launch_block(g, cus, (hipStream_t)stream));
 }
+// fused LN projections (k_block.hip lnproj): plain [N][256] bf16 weights; o != NULL: x' = x + o . Wo^T
+// stored to x, cp = LN(x') . Wp^T (np = 1); o == NULL: cp = LN(x) . Wp^T (np = 3), cr = x . Wr^T (nr = 0 / 2)
+int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* Wp, int np, const void* Wr, int nr,
+                    void* cp, void* cr, const float* gamma, const float* beta, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  void* p = nullptr;
+  const size_t n0 = 256 * 256, n1 = (size_t)np * 256 * 256, n2 = (size_t)nr * 256 * 256;
+  if (hipMalloc(&p, (n0 + n1 + n2 + 8) * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+  bf16 *p0 = (bf16*)p, *p1 = p0 + n0, *p2 = p1 + n1;
+  hipError_t e = hipSuccess;
+  if (Wo) e = launch_pack_rowpanel((const bf16*)Wo, p0, 256, 256, st);
+  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)Wp, p1, np * 256, 256, st);
+  if (e == hipSuccess && nr) e = launch_pack_rowpanel((const bf16*)Wr, p2, nr * 256, 256, st);
+  LnProjArgs g{};
+  g.x = x; g.o = (const bf16*)o; g.M = M; g.Wo = Wo ? p0 : nullptr; g.Wp = p1; g.Wr = nr ? p2 : nullptr;
+  g.cp = (bf16*)cp; g.ldp = np * 256; g.cr = (bf16*)cr; g.ldr = nr * 256;
+  g.gamma = gamma; g.beta = beta; g.eps = 1e-5f; g.np = np; g.nr = nr;
+  if (e == hipSuccess) e = launch_lnproj(g, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(p);
+  return rc_of(e);
+}
 int vap_test_read_block_stamps(unsigned long long* out) { return rc_of(read_block_stamps(out)); }
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
