@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Timeline of the last forward in a rocprofv3 kernel trace: every kernel of the last LSTM launch's
+window, start / end relative to the LSTM start (us), grouped by kernel class.
+
+    python tools/trace_timeline.py gpurun_out/prof_x/run_kernel_trace.csv
+"""
+import csv
+import sys
+
+
+def short(n):
+    for k in ("lstm_resident", "conv01", "gemm2_kernelIDF16b", "gemm2_kernel<float", "attn3", "block_kernel",
+              "lnproj_kernel", "rowpanel", "streamOpsWait", "streamOpsWrite", "probs", "labels", "vad_head",
+              "zero_rows", "copyBuffer", "layernorm"):
+        if k in n:
+            return k
+    return n[:40]
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"]) for r in rows]
+    ks.sort()
+    lstm = [k for k in ks if k[2] == "lstm_resident"]
+    L = lstm[-2] if len(lstm) > 1 else lstm[-1]  # the last timed forward (the very last may be a breakdown pass)
+    t0 = L[0]
+    win = [k for k in ks if k[0] >= L[0] - 3_000_000 and k[0] <= L[1] + 3_000_000]
+    prev_end = None
+    print(f"LSTM {L[0]-t0} .. {(L[1]-t0)/1e3:.1f} us (queue {L[3]})")
+    for s, e, n, q in win:
+        if n == "lstm_resident":
+            continue
+        gap = "" if prev_end is None else f" gap {(s - prev_end)/1e3:7.1f}"
+        print(f"{(s - t0)/1e3:9.1f} {(e - t0)/1e3:9.1f} {(e - s)/1e3:8.1f} q{q} {n}{gap}")
+        prev_end = e
+
+
+if __name__ == "__main__":
+    main()

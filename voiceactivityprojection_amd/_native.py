@@ -75,6 +75,7 @@ _SIGS = {
     "vap_test_read_rp_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_ffn_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_block_stamps": (ctypes.c_int, [_P]),
+    "vap_test_read_lnproj_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_gemm_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_lstm_stamps": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),

@@ -391,7 +391,12 @@ hipError_t read_block_stamps(unsigned long long* out) {
 // trades the two 16-column blocks between lane groups so a lane holds 8 consecutive columns.
 namespace {
 
-template <int MT, bool OPROJ, int NP, int NR>
+// diagnostics (VAP_LNPROJ_STAMPS=1): wave 0 of workgroups 0, 64, .., 448 records s_memtime at [0] start,
+// [1] O panel in LDS, [2] out-projection done, [3] LN panel complete, [4 + p] pass p's MFMAs done,
+// [10 + p] pass p's stores issued, [16] all stores complete
+__device__ unsigned long long g_lnp_stamps[8][24];
+
+template <int MT, bool OPROJ, int NP, int NR, bool ST = false>
 __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs g) {
   static_assert(!(OPROJ && NR), "the raw panel shares H with the O panel");
   using C = Blk<MT>;
@@ -408,6 +413,16 @@ __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = blockIdx.x * R;
   const int rps = g.rows_per_seq;
+  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && tid == 0) ? (int)(blockIdx.x >> 6) : -1;
+  unsigned long long stv[17] = {};  // wave-uniform: SGPRs
+  auto stamp = [&](int k) {
+    if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
+      stv[k] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp(0);
   auto roff = [&](int m, int64_t seq, int64_t ld) -> int64_t {
     if (rps == 0) return (int64_t)m * ld;
     const int sq = m / rps;
@@ -482,8 +497,10 @@ __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs
       *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = ot[k];
     }
     __syncthreads();
+    stamp(1);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) kstep(H, ks, ks, acc);
+    stamp(2);
     // x' back to HBM now (it is the residual the cross attention adds to)
 #pragma unroll
     for (int j = 0; j < MT; ++j)
@@ -507,6 +524,7 @@ __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs
   ln_panel<MT>(acc, red0, red1, GB, P, w, l16, lg, g.eps);
   __syncthreads();  // P (and the raw panel) complete
   __builtin_amdgcn_sched_barrier(0);
+  stamp(3);
 
   // ---------------------------------------------------------------- projections, one N tile per pass
 #pragma unroll
@@ -520,6 +538,7 @@ __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs
       for (int j = 0; j < MT; ++j) c[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) kstep(raw ? H : P, ks, Q0 + 8 * p + ks, c);
+    stamp(4 + p);
     bf16* out = raw ? g.cr : g.cp;
     const int64_t ld = raw ? g.ldr : g.ldp, seq = raw ? g.cr_seq : g.cp_seq;
     const int64_t cbase = roff(m0, seq, ld);
@@ -539,13 +558,28 @@ __global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs
       }
       buf_store16(rc, co[j] + col * 2u, u32x4{a[0], a[1], b[0], b[1]});
     }
+    stamp(10 + p);
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (ST) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(16);
+    if (samp >= 0)
+      for (int k = 0; k < 17; ++k) g_lnp_stamps[samp][k] = stv[k];
   }
 }
 
 template <int MT>
 hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
+  static const bool stamps = getenv("VAP_LNPROJ_STAMPS") != nullptr;
+  if (stamps) {
+    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, true>), grid, dim3(512), 0, st, g);
+    else if (!g.o && g.np == 3 && g.nr == 2)
+      hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, true>), grid, dim3(512), 0, st, g);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0>), grid, dim3(512), 0, st, g);
   else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0>), grid, dim3(512), 0, st, g);
   else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2>), grid, dim3(512), 0, st, g);
@@ -569,4 +603,8 @@ hipError_t launch_lnproj(const LnProjArgs& g, hipStream_t st) {
       (g.nr && span(g.cr_seq, g.ldr, 2) >= 0x7FFFFFF0LL) || (g.o && span(g.o_seq, D, 2) >= 0x7FFFFFF0LL))
     return hipErrorInvalidValue;
   return launch_lnproj_mt<4>(g, st);
+}
+
+hipError_t read_lnproj_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lnp_stamps), sizeof(g_lnp_stamps), 0, hipMemcpyDeviceToHost);
 }

@@ -54,6 +54,11 @@ struct vap_handle {
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
   bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
+  double tc_edge = 0.0;             // time chunks: first / last chunk fraction of the frames (0: even split)
+  // forward: front-end / back-end boundaries (cumulative frame fractions, VAP_TC_FE / VAP_TC_BE;
+  // "" = the even time_chunks split for both)
+  std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.4, 0.7, 0.9};
+  std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
   bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
                              // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
   bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
@@ -979,16 +984,93 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
 // earlier chunks' back ends, for all clips at once.
 // Time-chunk schedule of a plan: frame chunks [fb[c], fb[c+1]) and the LSTM step at which each ends.
 struct TcSched {
-  int nch = 1;
-  int fb[vap_handle::MAXMB + 1]{};
-  int seq_end[vap_handle::MAXMB]{};
+  int nch = 1;                          // recurrence chunks (ready / done hand-offs)
+  int fb[vap_handle::MAXMB + 1]{};      // their frame boundaries
+  int seq_end[vap_handle::MAXMB]{};     // LSTM step (conv4 row) at which each ends
+  bool fe_pub[vap_handle::MAXMB]{};     // the front end publishes after chunk c (else it runs on)
+  int nbe = 1;                          // back-end chunks: chunk k covers recurrence chunks
+  int be_end[vap_handle::MAXMB + 1]{};  // [be_end[k-1], be_end[k]) (be_end[-1] = 0)
 };
+// Chunk sizes: the step is bounded by the caller-stream work AND by the chain "front end of chunk 0
+// -> whole recurrence -> back end of the last chunk", so the first and last chunks are short (edge
+// fraction h->tc_edge of the frames each, >= 32 frames) and the middle ones share the rest evenly.
+// VAP_TC_SPLIT="w0,w1,.." sets explicit relative chunk sizes instead.
 TcSched tc_schedule(const vap_handle* h, const Plan& p) {
   TcSched t;
   const int T_ = p.T;
   t.nch = std::min(h->time_chunks, vap_handle::MAXMB);
   t.nch = std::max(1, std::min(t.nch, T_ / 32));  // chunks of at least 32 frames
-  for (int c = 0; c <= t.nch; ++c) t.fb[c] = (int)((int64_t)T_ * c / t.nch);
+  std::vector<double> wt;
+  if (!h->tc_split.empty()) {
+    for (double v : h->tc_split) wt.push_back(v);
+    if ((int)wt.size() > std::min(vap_handle::MAXMB, T_ / 32)) wt.clear();
+  }
+  if (wt.empty()) {
+    wt.assign(t.nch, 1.0);
+    if (t.nch >= 3 && h->tc_edge > 0.0) {
+      const double e = std::max(h->tc_edge, 32.0 / T_);
+      const double mid = (1.0 - 2 * e) / (t.nch - 2);
+      if (mid * T_ >= 32) {
+        for (int c = 0; c < t.nch; ++c) wt[c] = (c == 0 || c == t.nch - 1) ? e : mid;
+      }
+    }
+  }
+  t.nch = (int)wt.size();
+  double tot = 0;
+  for (double v : wt) tot += v;
+  double acc = 0;
+  t.fb[0] = 0;
+  for (int c = 0; c < t.nch; ++c) {
+    acc += wt[c];
+    t.fb[c + 1] = c + 1 == t.nch ? T_ : std::max(t.fb[c] + 1, std::min(T_ - (t.nch - c - 1), (int)(T_ * acc / tot + 0.5)));
+  }
+  for (int c = 0; c < t.nch; ++c)
+    t.seq_end[c] = c + 1 == t.nch ? (int)p.L[4] : std::min((int)p.L[4], 2 * t.fb[c + 1]);
+  t.nbe = t.nch;
+  for (int c = 0; c < t.nch; ++c) {
+    t.fe_pub[c] = true;
+    t.be_end[c] = c + 1;
+  }
+  return t;
+}
+
+// Forward schedule with separate front-end and back-end chunkings (h->tc_fe / h->tc_be: cumulative
+// frame fractions of the boundaries, 1 excluded).  The step is bounded by the caller-stream work and
+// by the chain "front end up to the first hand-off -> the whole recurrence -> back end after the last
+// hand-off": the front end publishes in growing pieces (a short first one starts the recurrence early,
+// each later one is ready before the recurrence gets there: the front end runs ~1.4x faster per
+// frame than the recurrence), the back end works in shrinking pieces (a short last one after the
+// recurrence ends).  The recurrence hands off at the union of both boundary sets.
+TcSched tc_schedule_split(const vap_handle* h, const Plan& p) {
+  const int T_ = p.T;
+  if (h->tc_fe.empty() || h->tc_be.empty() || T_ < 128) return tc_schedule(h, p);
+  std::vector<std::tuple<int, bool, bool>> bd;  // frame, front-end boundary, back-end boundary
+  for (double f : h->tc_fe) bd.emplace_back((int)(T_ * f + 0.5), true, false);
+  for (double f : h->tc_be) bd.emplace_back((int)(T_ * f + 0.5), false, true);
+  std::sort(bd.begin(), bd.end());
+  std::vector<std::tuple<int, bool, bool>> m;  // merged: boundaries closer than 24 frames become one
+  for (auto& b : bd) {
+    int f = std::get<0>(b);
+    if (f < 24 || f > T_ - 24) continue;
+    if (!m.empty() && f - std::get<0>(m.back()) < 24) {
+      std::get<0>(m.back()) = f;
+      std::get<1>(m.back()) = std::get<1>(m.back()) || std::get<1>(b);
+      std::get<2>(m.back()) = std::get<2>(m.back()) || std::get<2>(b);
+    } else {
+      m.push_back(b);
+    }
+  }
+  m.emplace_back(T_, true, true);
+  if ((int)m.size() > vap_handle::MAXMB) return tc_schedule(h, p);
+  TcSched t;
+  t.nch = (int)m.size();
+  t.fb[0] = 0;
+  t.nbe = 0;
+  for (int c = 0; c < t.nch; ++c) {
+    t.fb[c + 1] = std::get<0>(m[c]);
+    t.fe_pub[c] = std::get<1>(m[c]);
+    if (std::get<2>(m[c])) t.be_end[t.nbe++] = c + 1;
+  }
   for (int c = 0; c < t.nch; ++c)
     t.seq_end[c] = c + 1 == t.nch ? (int)p.L[4] : std::min((int)p.L[4], 2 * t.fb[c + 1]);
   return t;
@@ -1036,8 +1118,9 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     HIPCHK(hipStreamWaitEvent(bst, fk, 0));
   }
   int rc;
-  for (int c = 0; c < t.nch; ++c) {
-    const int f0 = t.fb[c], f1 = t.fb[c + 1];
+  for (int k = 0; k < t.nbe; ++k) {
+    const int c = t.be_end[k] - 1;  // the last recurrence chunk of back-end chunk k
+    const int f0 = t.fb[k ? t.be_end[k - 1] : 0], f1 = t.fb[c + 1];
     if (kernel_expect)  // captured streaming push: the hand-off as a kernel (graph-capturable)
       HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bst));
     else
@@ -1139,16 +1222,18 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
 int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, float* logits, float* vadl,
                    unsigned char* ws, hipStream_t st) {
   using T = bf16;
-  const TcSched t = tc_schedule(h, p);
+  const TcSched t = tc_schedule_split(h, p);
   T* GX = (T*)(ws + p.GX);
   LstmSync sy;
   int rc;
   if ((rc = tc_launch_lstm(h, p, t, GX, ws, sy, st))) return rc;
   int64_t done_rows = 0;
-  for (int c = 0; c < t.nch; ++c) {  // front end, chunk by chunk
+  int published = 0;
+  for (int c = 0; c < t.nch; ++c) {  // front end, piece by piece (a piece ends at a front-end boundary)
+    if (!t.fe_pub[c]) continue;
     if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st))) return rc;
     done_rows = t.seq_end[c];
-    HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + c), sy.epoch, 0));
+    for (; published <= c; ++published) HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published), sy.epoch, 0));
   }
   return tc_back_end(h, p, t, sy, ws, logits, vadl, st);
 }
@@ -1372,7 +1457,7 @@ int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, floa
   const int nxt = 1 - s->cur;
   const int64_t L4 = p.L[4];
   const int64_t off = (s->gx_off + s->hop_rows) % L4;
-  const TcSched t = tc_schedule(h, p);
+  const TcSched t = tc_schedule_split(h, p);
   // eager: stage the hop, zero the hand-off words, start the recurrence on the side stream
   HIPCHK(hipMemcpyAsync(s->hop_buf, hop_audio, (size_t)S * s->hop * sizeof(float), hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemsetAsync(s->gsync, 0, (2 * vap_handle::MAXMB + 1) * sizeof(unsigned), st));
@@ -1454,7 +1539,7 @@ int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad
   bf16* GX = s->gx;
   // the window moved by hop_rows conv4 rows: carried rows keep their ring slots
   const int64_t off = s->pushes > 0 ? (s->gx_off + s->hop_rows) % L4 : 0;
-  const TcSched t = tc_schedule(h, p);
+  const TcSched t = tc_schedule_split(h, p);
   LstmSync sy;
   if ((rc = tc_launch_lstm(h, p, t, GX, s->ws, sy, st, (int)off))) return rc;
   int published = 0;
@@ -1531,6 +1616,32 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);
+  if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
+  auto parse_list = [](const char* e, std::vector<double>& out) {
+    out.clear();
+    std::string v = e;
+    size_t a = 0;
+    while (a < v.size()) {
+      size_t b = v.find(',', a);
+      if (b == std::string::npos) b = v.size();
+      const double x = atof(v.substr(a, b - a).c_str());
+      if (x > 0 && x < 1) out.push_back(x);
+      a = b + 1;
+    }
+  };
+  if (const char* e = getenv("VAP_TC_FE")) parse_list(e, h->tc_fe);
+  if (const char* e = getenv("VAP_TC_BE")) parse_list(e, h->tc_be);
+  if (const char* e = getenv("VAP_TC_SPLIT")) {
+    std::string v = e;
+    size_t a = 0;
+    while (a < v.size()) {
+      size_t b = v.find(',', a);
+      if (b == std::string::npos) b = v.size();
+      const double x = atof(v.substr(a, b - a).c_str());
+      if (x > 0) h->tc_split.push_back(x);
+      a = b + 1;
+    }
+  }
   if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);

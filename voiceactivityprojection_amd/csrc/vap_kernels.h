@@ -217,3 +217,4 @@ struct LnProjArgs {
   int np, nr;
 };
 hipError_t launch_lnproj(const LnProjArgs& g, hipStream_t st);
+hipError_t read_lnproj_stamps(unsigned long long* out);

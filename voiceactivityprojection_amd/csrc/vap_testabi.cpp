@@ -191,6 +191,7 @@ int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* 
   (void)hipFree(p);
   return rc_of(e);
 }
+int vap_test_read_lnproj_stamps(unsigned long long* out) { return rc_of(read_lnproj_stamps(out)); }
 int vap_test_read_block_stamps(unsigned long long* out) { return rc_of(read_block_stamps(out)); }
 int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
 int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
