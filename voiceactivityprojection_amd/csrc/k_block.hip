@@ -334,6 +334,15 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
         buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+    if (g.xb) {  // bf16 copy (the combinator's input after the last layer): same rows, half the bytes
+      const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.xb + xbase, 0x7FFFFFF0u);
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          buf_store8(rb, ((xo[j] >> 1) | (xo[j] & 0x80000000u)) + (uint32_t)(w * 32 + i * 16 + lg * 4) * 2u,
+                     pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
+    }
   }
   if constexpr (ST) {
     stamp(16);

@@ -131,6 +131,31 @@ __global__ __launch_bounds__(256) void vad_head_kernel(const float* __restrict__
   }
 }
 
+// frame range variant (time-chunked back end): row over (seq, t in [t0, t0 + nt))
+__global__ __launch_bounds__(256) void vad_head_rows_kernel(const float* __restrict__ x, int64_t x_seq, int B, int Tn,
+                                                           int t0, int nt, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, float* __restrict__ vad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)2 * B * nt) return;
+  const int64_t s = row / nt, t = row - s * nt;
+  const f32x4 v = *(const f32x4*)(x + s * x_seq + t * 256 + lane * 4);
+  const f32x4 ww = *(const f32x4*)(w + lane * 4);
+  const float d = wave_sum(v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3]) + bias[0];
+  if (lane == 0) vad[((s >> 1) * Tn + t0 + t) * 2 + (s & 1)] = d;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restrict__ in, int64_t in_seq,
+                                                          T* __restrict__ out, int64_t out_seq, int n_seq, int rows) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // 4 elements each
+  const int64_t per_seq = (int64_t)rows * 64;
+  if (i >= per_seq * n_seq) return;
+  const int64_t s = i / per_seq, e = (i - s * per_seq) * 4;
+  const f32x4 v = *(const f32x4*)(in + s * in_seq + e);
+  store4(out + s * out_seq + e, v[0], v[1], v[2], v[3]);
+}
+
 // ------------------------------------------------------------------------------------------
 // probs() epilogue (model.py:189-213): softmax, sigmoid VAD, entropy H = sum -p log2 p, and
 // probs_next_speaker_aggregate (objective.py:184-204) for the now / future bin ranges:
@@ -329,6 +354,27 @@ hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const 
   hipLaunchKernelGGL(vad_head_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, B, Tn, w, bias, vad);
   return hipGetLastError();
 }
+
+hipError_t launch_vad_head_rows(const float* x, int64_t x_seq, int B, int Tn, int t0, int nt, const float* w,
+                                const float* bias, float* vad, hipStream_t st) {
+  if (B <= 0 || nt <= 0 || t0 < 0 || t0 + nt > Tn) return hipErrorInvalidValue;
+  const int64_t rows = (int64_t)2 * B * nt;
+  hipLaunchKernelGGL(vad_head_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, x_seq, B, Tn, t0, nt,
+                     w, bias, vad);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_convert_rows(const float* in, int64_t in_seq, T* out, int64_t out_seq, int n_seq, int rows,
+                               hipStream_t st) {
+  if (n_seq <= 0 || rows <= 0) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)n_seq * rows * 64;
+  hipLaunchKernelGGL((convert_rows_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, in_seq, out,
+                     out_seq, n_seq, rows);
+  return hipGetLastError();
+}
+template hipError_t launch_convert_rows<float>(const float*, int64_t, float*, int64_t, int, int, hipStream_t);
+template hipError_t launch_convert_rows<bf16>(const float*, int64_t, bf16*, int64_t, int, int, hipStream_t);
 
 hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
                         int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,

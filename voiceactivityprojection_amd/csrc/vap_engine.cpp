@@ -59,6 +59,7 @@ struct vap_handle {
   // "" = the even time_chunks split for both)
   std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.4, 0.7, 0.9};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
+  bool heads_chunked = true;  // time-chunked back end: heads per chunk (VAP_HEADS_CHUNKED=0: once at the end)
   bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
                              // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
   bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
@@ -872,7 +873,7 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
 // Q/K/V (self) and K/V (cross) live in per-layer buffers so later chunks attend to earlier ones:
 // attention is causal, so queries [f0, f1) need keys [0, f1) only (modules.py:169-202).
 int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, int li, int ci,
-                int f0, int f1, hipStream_t st) {
+                int f0, int f1, hipStream_t st, bf16* xb_out = nullptr) {
   using T = bf16;
   const int T_ = p.T, S = p.S, nf = f1 - f0;
   const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
@@ -957,6 +958,7 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       BlockArgs b{Xf, ATT + (int64_t)f0 * D, S * nf, nf, t1, t1, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")),
                   h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                   h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+      b.xb = xb_out ? xb_out + (int64_t)f0 * D : nullptr;
       HIPCHK(launch_block(b, 0, st));
     } else if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
       FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
@@ -1100,6 +1102,43 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
   return VAP_OK;
 }
 
+// Heads on frames [f0, f1) of every clip (stereo, time-chunked back end): combinator (two GEMMs with
+// the shared LN + GELU epilogue, the second adding onto the first), vap_head, va_classifier -- all
+// row-wise (modules.py:411-449, model.py:257-261), so each back-end chunk finishes its own heads and
+// only the last chunk's remain after the recurrence.  RAW holds the bf16 copy of the final x that
+// the last layer's block kernel wrote.
+int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, float* logits, float* vadl,
+             hipStream_t st) {
+  using T = bf16;
+  const int T_ = p.T, nf = f1 - f0, B = p.B;
+  const int64_t t1 = (int64_t)T_ * D;
+  float* X = (float*)(ws + p.X);
+  T* RAW = (T*)(ws + p.RAW);
+  float* HC = (float*)(ws + p.HC);
+  T* HCT = (T*)(ws + p.HCT);
+  Timed tm(h, VAP_K_HEADS, st);
+  const int64_t o = (int64_t)f0 * D;
+  GemmArgs ga = gargs(RAW + o, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, nf, B, HC + o, D, t1);
+  ga.norm = 2;
+  ga.act = 2;
+  ga.gamma = h->P("ar.combinator.ln.weight");
+  ga.beta = h->P("ar.combinator.ln.bias");
+  HIPCHK(gemm<T>(ga, st, true));
+  GemmArgs gb = ga;
+  gb.A = RAW + t1 + o;
+  gb.W = h->W<T>("comb_b");
+  gb.add = HC + o;
+  gb.ld_add = D;
+  gb.add_seq_stride = t1;
+  HIPCHK(gemm<T>(gb, st, true));
+  HIPCHK(launch_convert_rows<T>(HC + o, t1, HCT + o, t1, B, nf, st));
+  HIPCHK(gemm<T>(gargs(HCT + o, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), nf, B,
+                       logits + (int64_t)f0 * 256, 256, (int64_t)T_ * 256), st, true));
+  HIPCHK(launch_vad_head_rows(X + o, t1, B, T_, f0, nf, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
+                              vadl, st));
+  return VAP_OK;
+}
+
 // Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
 // every transformer layer on the chunk's frames; then heads over all clips and the join.
 int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& sy, unsigned char* ws, float* logits,
@@ -1135,13 +1174,20 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       ga.beta = h->P("encoder.downsample.2.ln.bias");
       HIPCHK(gemm<T>(ga, bst, true));
     }
+    // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
+    const bool hchunk = h->heads_chunked && h->block_fused && h->ffn_fused && h->dims.cross_layers > 0;
     int li = 0;
     for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
       if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, bst))) return rc;
-    for (int l = 0; l < h->dims.cross_layers; ++l, ++li)
-      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst))) return rc;
+    for (int l = 0; l < h->dims.cross_layers; ++l, ++li) {
+      bf16* xb = hchunk && l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
+      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst, xb))) return rc;
+    }
+    if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bst))) return rc;
   }
-  if ((rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst))) return rc;
+  if (!(h->heads_chunked && h->block_fused && h->ffn_fused && h->dims.cross_layers > 0) &&
+      (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst)))
+    return rc;
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
@@ -1613,6 +1659,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_FFN_FUSED")) h->ffn_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_BLOCK")) h->block_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_LNPROJ")) h->lnproj_fused = atoi(e) != 0;
+  if (const char* e = getenv("VAP_HEADS_CHUNKED")) h->heads_chunked = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);

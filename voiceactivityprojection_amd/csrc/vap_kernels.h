@@ -100,6 +100,13 @@ hipError_t launch_attn_probs(const AttnArgs& a, float* out, int64_t out_seq, int
 
 // va_classifier on both towers: vad[b][t][c] = dot(x[2b+c][t], w) + bias (x fp32, clip-major seqs)
 hipError_t launch_vad_head(const float* x, int B, int Tn, const float* w, const float* bias, float* vad, hipStream_t st);
+// frames [t0, t0 + nt) of every sequence: x points at frame t0 of sequence 0, sequences x_seq apart
+hipError_t launch_vad_head_rows(const float* x, int64_t x_seq, int B, int Tn, int t0, int nt, const float* w,
+                                const float* bias, float* vad, hipStream_t st);
+// rows [0, rows) of n_seq sequences of 256-wide fp32 rows -> T (sequence strides in elements)
+template <typename T>
+hipError_t launch_convert_rows(const float* in, int64_t in_seq, T* out, int64_t out_seq, int n_seq, int rows,
+                               hipStream_t st);
 
 hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
                         int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,
@@ -192,6 +199,7 @@ struct BlockArgs {
   const float* gamma;
   const float* beta;
   float eps;
+  bf16* xb = nullptr;  // optional bf16 copy of the output rows (same row layout as x)
 };
 hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);
