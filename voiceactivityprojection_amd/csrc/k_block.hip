@@ -32,7 +32,9 @@ namespace {
 
 constexpr int D = 256;
 constexpr int ROWB = D * 2;  // bf16 row of the panel / of a hidden slice: 512 B = 32 chunks
-constexpr int NPF = 2;       // weight prefetch depth (k-steps)
+// weight prefetch depth NPF (k-steps, a template parameter): a 64-row k-step is only ~256 MFMA
+// cycles per SIMD, so 2 in flight leave the L2 round trip exposed; 8 in flight cost 48 VGPRs,
+// which drops the 64-row kernels from two workgroups per CU to one
 
 template <int MT> struct Blk {
   static constexpr int R = 16 * MT;
@@ -144,7 +146,7 @@ VAP_DEV void ln_panel(const f32x4 (&acc)[2][MT], float* red0, float* red1, const
 // issued, [17] stores complete
 __device__ unsigned long long g_blk_stamps[8][24];
 
-template <int MT, bool OPROJ, bool ST = false>
+template <int MT, bool OPROJ, bool ST = false, int NPF = 2>
 __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   using C = Blk<MT>;
   constexpr int R = C::R;
@@ -357,7 +359,10 @@ template <int MT>
 hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
   static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
-  if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
+  static const int npf = getenv("VAP_BLOCK_NPF") ? atoi(getenv("VAP_BLOCK_NPF")) : 2;
+  if (stamps && g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, true, 8>), grid, dim3(512), 0, st, g);
+  else if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
+  else if (g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, false, 8>), grid, dim3(512), 0, st, g);
   else if (g.o) hipLaunchKernelGGL((block_kernel<MT, true>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((block_kernel<MT, false>), grid, dim3(512), 0, st, g);
   return hipGetLastError();
@@ -405,8 +410,8 @@ namespace {
 // [10 + p] pass p's stores issued, [16] all stores complete
 __device__ unsigned long long g_lnp_stamps[8][24];
 
-template <int MT, bool OPROJ, int NP, int NR, bool ST = false>
-__global__ __launch_bounds__(512, MT <= 4 ? 4 : 2) void lnproj_kernel(LnProjArgs g) {
+template <int MT, bool OPROJ, int NP, int NR, bool ST = false, int NPF = 2>
+__global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
   static_assert(!(OPROJ && NR), "the raw panel shares H with the O panel");
   using C = Blk<MT>;
   constexpr int R = C::R;
@@ -586,6 +591,14 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
     if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, true>), grid, dim3(512), 0, st, g);
     else if (!g.o && g.np == 3 && g.nr == 2)
       hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, true>), grid, dim3(512), 0, st, g);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  static const int npf = getenv("VAP_LNPROJ_NPF") ? atoi(getenv("VAP_LNPROJ_NPF")) : 2;
+  if (npf == 8) {
+    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, 8>), grid, dim3(512), 0, st, g);
+    else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, 8>), grid, dim3(512), 0, st, g);
+    else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, false, 8>), grid, dim3(512), 0, st, g);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
