@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--S", type=int, default=128)
     ap.add_argument("--T", type=int, default=2000)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--variant", type=int, default=2, help="0 resident, 2 resident pre-scaled (the engine's)")
     args = ap.parse_args()
     lib = N.lib()
     dev = torch.device("cuda", 0)
@@ -30,12 +31,12 @@ def main():
     out = torch.empty(S, T, 256, dtype=torch.bfloat16, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())
-    N.check(lib.vap_test_lstm(1, P(gx), S, T, P(whh), P(whp), P(out), 0, st))
+    N.check(lib.vap_test_lstm(1, P(gx), S, T, P(whh), P(whp), P(out), args.variant, st))
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.iters):
-        N.check(lib.vap_test_lstm(1, P(gx), S, T, P(whh), P(whp), P(out), 0, st))
+        N.check(lib.vap_test_lstm(1, P(gx), S, T, P(whh), P(whp), P(out), args.variant, st))
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters

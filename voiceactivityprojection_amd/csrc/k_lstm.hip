@@ -149,10 +149,23 @@ VAP_DEV void mfma_v(f32x4& c, const chunk16& a, const chunk16& b) {
 }
 
 // One cell of the LSTM update for register r of a finished unit tile.
+// PRE: the gate pre-activations arrive pre-scaled (W_ih, W_hh, biases packed with -log2e on the i / f
+// / o rows and 2 log2e on the g rows), and c is kept as 2 log2e c, so every activation is
+// exp2 + add + rcp with no argument scaling: 10 VALU + 10 transcendentals per cell instead of 15 + 10.
+constexpr float KC = 2.8853900817779268f;  // 2 log2(e)
+template <bool PRE>
 VAP_DEV void lstm_cell(const f32x4 (&acc)[4], int r, float& c, float& h) {
-  const float ig = fsig(acc[0][r]), fg = fsig(acc[1][r]), gg = ftanh(acc[2][r]), og = fsig(acc[3][r]);
-  c = fg * c + ig * gg;
-  h = og * ftanh(c);
+  if constexpr (PRE) {
+    auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x)); };  // sigmoid(-x ln2)
+    const float ig = sg(acc[0][r]), fg = sg(acc[1][r]), og = sg(acc[3][r]);
+    const float gk = __builtin_fmaf(-2.0f * KC, sg(acc[2][r]), KC);  // 2 log2e tanh(g), acc = 2 log2e g
+    c = fg * c + ig * gk;                                               // 2 log2e c
+    h = og * __builtin_fmaf(-2.0f, sg(c), 1.0f);                        // tanh(c) = 1 - 2 / (1 + 2^{c'})
+  } else {
+    const float ig = fsig(acc[0][r]), fg = fsig(acc[1][r]), gg = ftanh(acc[2][r]), og = fsig(acc[3][r]);
+    c = fg * c + ig * gg;
+    h = og * ftanh(c);
+  }
 }
 
 // LDS operands of one k-step q = ut*8 + kg: the h fragment and the LDS-resident weight fragments
@@ -191,7 +204,7 @@ struct LstmState {
 // k-step Q of the step: issue the LDS reads of step Q+1, then the four MFMAs of step Q; the cell
 // update of the previous unit tile is interleaved (one register per two k-steps) so the vector
 // and matrix pipes of the SIMD overlap.
-template <int Q>
+template <int Q, bool PRE>
 VAP_DEV void kstep(LstmState& st, const KPre& cur, KPre& nxt, const bf16* gt, const chunk16 (&wa)[R_NAGPR],
                    const chunk16 (&wv)[R_NVGPR], const chunk16* wl, const unsigned char* hb, int sl, int lane) {
   constexpr int UT = Q >> 3, KG = Q & 7;
@@ -214,7 +227,7 @@ VAP_DEV void kstep(LstmState& st, const KPre& cur, KPre& nxt, const bf16* gt, co
     if constexpr (KG == 1)  // consumers of the previous tile stay below this point (no MFMA->VALU hazard)
       asm volatile("" : "+v"(st.prev[0]), "+v"(st.prev[1]), "+v"(st.prev[2]), "+v"(st.prev[3]));
     if constexpr (KG & 1) {
-      lstm_cell(st.prev, KG >> 1, st.c[UT - 1][KG >> 1], st.hv[UT - 1][KG >> 1]);
+      lstm_cell<PRE>(st.prev, KG >> 1, st.c[UT - 1][KG >> 1], st.hv[UT - 1][KG >> 1]);
       // pin the cell here, between this k-step's MFMAs and the next's (all volatile asm): left
       // alone the compiler sinks every cell update to the h write after the step's MFMAs, so the
       // transcendental work never overlaps the matrix pipe
@@ -226,23 +239,23 @@ VAP_DEV void kstep(LstmState& st, const KPre& cur, KPre& nxt, const bf16* gt, co
     for (int g = 0; g < 4; ++g) st.prev[g] = st.acc[g];
     if constexpr (UT == 3) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) lstm_cell(st.prev, r, st.c[3][r], st.hv[3][r]);
+      for (int r = 0; r < 4; ++r) lstm_cell<PRE>(st.prev, r, st.c[3][r], st.hv[3][r]);
     }
   }
 }
 
-template <int Q>
+template <int Q, bool PRE>
 VAP_DEV void ksteps(LstmState& st, KPre& cur, KPre& nxt, const bf16* gt, const chunk16 (&wa)[R_NAGPR],
                     const chunk16 (&wv)[R_NVGPR], const chunk16* wl, const unsigned char* hb, int sl, int lane) {
-  kstep<Q>(st, cur, nxt, gt, wa, wv, wl, hb, sl, lane);
-  if constexpr (Q + 1 < 32) ksteps<Q + 1>(st, nxt, cur, gt, wa, wv, wl, hb, sl, lane);
+  kstep<Q, PRE>(st, cur, nxt, gt, wa, wv, wl, hb, sl, lane);
+  if constexpr (Q + 1 < 32) ksteps<Q + 1, PRE>(st, nxt, cur, gt, wa, wv, wl, hb, sl, lane);
 }
 
 // diagnostics (VAP_LSTM_STAMPS=1): wave 0 of workgroups 0..7 records s_memtime at steps 100..103:
 // [step start, k-steps + cell done, after barrier 1, h written, after barrier 2]
 __device__ unsigned long long g_lstm_stamps[8][4][5];
 
-template <bool ST>
+template <bool ST, bool PRE>
 __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __restrict__ gx, int S, int Tn,
                                                               const chunk16* __restrict__ wp, bf16* __restrict__ out,
                                                               int64_t out_seq_stride, LstmSync sync) {
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
     const bf16* gt = gxs + grow(t + 1 < Tn ? t + 1 : t);
     stamp(t, 0);
     kload<0>(pa, wl, hb, sl, lane);
-    ksteps<0>(st, pa, pb, gt, wa, wv, wl, hb, sl, lane);
+    ksteps<0, PRE>(st, pa, pb, gt, wa, wv, wl, hb, sl, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stamp(t, 1);
     __builtin_amdgcn_s_barrier();  // every wave has consumed h_{t-1} (no vmcnt drain: gx prefetch stays in flight)
@@ -379,7 +392,10 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
 }
 
 // Wp[w][f = rt*8 + kg][lane][e] = W[g*256 + 64w + 16ut + (l&15)][32kg + 8(l>>4) + e],  rt = g*4 + ut
-__global__ void pack_whh_resident_kernel(const float* __restrict__ whh, bf16* __restrict__ out) {
+// gate-row scale of the pre-scaled packing (lstm_cell<true>): -log2e on i / f / o, 2 log2e on g
+VAP_DEV float gate_scale(int row) { return (row >> 8) == 2 ? KC : -0.5f * KC; }
+
+__global__ void pack_whh_resident_kernel(const float* __restrict__ whh, bf16* __restrict__ out, int pre) {
   const int64_t n = (int64_t)G4 * HD;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int e = (int)(i & 7);
@@ -389,11 +405,34 @@ __global__ void pack_whh_resident_kernel(const float* __restrict__ whh, bf16* __
     const int rt = f >> 3, kg = f & 7, g = rt >> 2, ut = rt & 3;
     const int row = g * HD + 64 * w + 16 * ut + (l & 15);
     const int k = 32 * kg + 8 * (l >> 4) + e;
-    out[i] = (bf16)whh[(int64_t)row * HD + k];
+    out[i] = (bf16)(whh[(int64_t)row * HD + k] * (pre ? gate_scale(row) : 1.0f));
   }
 }
 
+// W_ih [1024][256] fp32 -> bf16 with the gate-row scales; b = (b_ih + b_hh) * scale
+__global__ void pack_wih_prescaled_kernel(const float* __restrict__ wih, bf16* __restrict__ out,
+                                          const float* __restrict__ bih, const float* __restrict__ bhh,
+                                          float* __restrict__ b) {
+  const int64_t n = (int64_t)G4 * HD;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / HD);
+    out[i] = (bf16)(wih[i] * gate_scale(row));
+    if (i < G4) b[i] = (bih[i] + bhh[i]) * gate_scale((int)i);
+  }
+}
+
+__global__ void scale_gates_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (bf16)((float)in[i] * gate_scale((int)(i & (G4 - 1))));
+}
+
 }  // namespace
+
+// gx rows [.][1024] -> the pre-scaled gate units of lstm_cell<true> (kernel tests)
+hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(scale_gates_kernel, dim3(1024), dim3(256), 0, st, in, out, n);
+  return hipGetLastError();
+}
 
 template <typename T>
 hipError_t launch_lstm(const float* gx, int S, int Tn, const T* whh_packed, T* out, int64_t out_seq_stride,
@@ -411,7 +450,7 @@ hipError_t launch_pack_whh(const float* whh, T* packed, hipStream_t st) {
 }
 
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
-                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync) {
+                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, bool prescaled) {
   if (S <= 0 || Tn <= 0) return hipErrorInvalidValue;
   LstmSync sy{};
   if (sync) {
@@ -423,16 +462,21 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
     sy = *sync;
   }
   static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
-  if (stamps)
-    hipLaunchKernelGGL(lstm_resident_kernel<true>, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
-                     (const chunk16*)whh_packed, out, out_seq_stride, sy);
-  else
-    hipLaunchKernelGGL(lstm_resident_kernel<false>, dim3((S + NS - 1) / NS), dim3(256), 0, st, gx, S, Tn,
-                     (const chunk16*)whh_packed, out, out_seq_stride, sy);
+  const dim3 grid((S + NS - 1) / NS);
+  const chunk16* wpk = (const chunk16*)whh_packed;
+  if (stamps && prescaled) hipLaunchKernelGGL((lstm_resident_kernel<true, true>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
+  else if (stamps) hipLaunchKernelGGL((lstm_resident_kernel<true, false>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
+  else if (prescaled) hipLaunchKernelGGL((lstm_resident_kernel<false, true>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
+  else hipLaunchKernelGGL((lstm_resident_kernel<false, false>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
   return hipGetLastError();
 }
-hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st) {
-  hipLaunchKernelGGL(pack_whh_resident_kernel, dim3(256), dim3(256), 0, st, whh, packed);
+hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st, bool prescaled) {
+  hipLaunchKernelGGL(pack_whh_resident_kernel, dim3(256), dim3(256), 0, st, whh, packed, prescaled ? 1 : 0);
+  return hipGetLastError();
+}
+hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,
+                                     hipStream_t st) {
+  hipLaunchKernelGGL(pack_wih_prescaled_kernel, dim3(256), dim3(256), 0, st, wih, packed, bih, bhh, bias);
   return hipGetLastError();
 }
 

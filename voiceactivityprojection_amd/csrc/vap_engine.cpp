@@ -446,12 +446,15 @@ int pack_all(vap_handle* h, hipStream_t st) {
     float* b = nullptr;
     if (!wih || !whh || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
     h->fpacked["bias" + s] = b;
-    HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
-    if constexpr (sizeof(T) == 2)
-      HIPCHK(launch_pack_whh_resident(h->P(p + "weight_hh" + s), whh, st));
-    else
+    if constexpr (sizeof(T) == 2) {  // resident bf16 recurrence: gate scales folded into the weights
+      HIPCHK(launch_pack_wih_prescaled(h->P(p + "weight_ih" + s), (bf16*)wih, h->P(p + "bias_ih" + s),
+                                       h->P(p + "bias_hh" + s), b, st));
+      HIPCHK(launch_pack_whh_resident(h->P(p + "weight_hh" + s), (bf16*)whh, st, true));
+    } else {
+      HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
       HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
-    HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
+      HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
+    }
   }
   {
     T* w = alloc("down", D * D * 5);
@@ -774,7 +777,7 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
     Timed tm(h, VAP_K_LSTM_REC, rec_st);
     if constexpr (bf)
       HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L4, (const bf16*)h->W<T>("whh" + s),
-                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr));
+                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr, true));
     else
       HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
   }
@@ -1098,7 +1101,7 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
   Timed tm(h, VAP_K_LSTM_REC, side);
-  HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy));
+  HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, true));
   return VAP_OK;
 }
 
@@ -1362,7 +1365,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       {
         Timed tm(h, VAP_K_LSTM_REC, side);
         HIPCHK(launch_lstm_resident((const bf16*)(ws + p.GX), S, (int)L[4], (const bf16*)h->W<T>("whh_l0"),
-                                    (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh, side, &sy));
+                                    (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh, side, &sy, true));
       }
       for (int i = 0; i < nr; ++i) {
         if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
@@ -1522,7 +1525,7 @@ int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, floa
   hipEvent_t fork = h->next_fork_event();
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
-  HIPCHK(launch_lstm_resident(s->gx, S, (int)L4, h->W<bf16>("whh_l0"), (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy));
+  HIPCHK(launch_lstm_resident(s->gx, S, (int)L4, h->W<bf16>("whh_l0"), (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy, true));
   // captured: everything else on the caller's stream
   const vap_stream::GKey key{off, nxt, logits, vadl};
   auto it = s->graphs.find(key);

@@ -76,9 +76,14 @@ struct LstmSync {
   int time_mode;
   int gx_off = 0;    // gate rows form a ring: step t reads gx row (t + gx_off) mod Tn (streaming)
 };
+// prescaled: W_ih / W_hh / biases packed with the gate scales (launch_pack_wih_prescaled,
+// launch_pack_whh_resident(.., true)): gates arrive as -log2e (i, f, o) / 2 log2e (g) multiples
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
-                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync);
-hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st);
+                                int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, bool prescaled = false);
+hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st, bool prescaled = false);
+hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st);
+hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,
+                                     hipStream_t st);
 
 struct AttnArgs {
   const void* Q; int64_t q_ld, q_seq;     // head h at column h*64

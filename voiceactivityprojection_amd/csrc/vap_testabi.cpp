@@ -75,6 +75,19 @@ int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq
 int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh, void* whh_packed, void* out,
                   int variant, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (precision == VAP_PRECISION_BF16 && variant == 2) {  // the engine's pre-scaled resident path
+    void* gs = nullptr;
+    const int64_t n = (int64_t)S * T * 1024;
+    if (hipMalloc(&gs, n * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+    hipError_t e = launch_pack_whh_resident(whh, (bf16*)whh_packed, st, true);
+    if (e == hipSuccess) e = launch_scale_gates((const bf16*)gx, (bf16*)gs, n, st);
+    if (e == hipSuccess)
+      e = launch_lstm_resident((const bf16*)gs, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr,
+                               true);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(gs);
+    return rc_of(e);
+  }
   if (precision == VAP_PRECISION_BF16 && variant == 0) {
     hipError_t e = launch_pack_whh_resident(whh, (bf16*)whh_packed, st);
     if (e != hipSuccess) return VAP_ERR_HIP;
