@@ -209,13 +209,15 @@ int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const
 int vap_test_read_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled fused-block workgroups (VAP_BLOCK_STAMPS=1) */
 int vap_test_read_block_stamps(unsigned long long* out);
+/* timing diagnostics: 8 x 24 s_memtime stamps of sampled LN-projection workgroups (VAP_LNPROJ_STAMPS=1) */
+int vap_test_read_lnproj_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 32 s_memtime stamps of sampled row-panel workgroups (VAP_RP_STAMPS=1) */
 int vap_test_read_rp_stamps(unsigned long long* out);
 /* timing diagnostics (VAP_FFN_STAMPS=1): 8 x 24 s_memtime stamps of sampled fused-FFN workgroups, then
  * 1024 x 2 s_memrealtime start / end of every workgroup (out holds 2240 values) */
 int vap_test_read_ffn_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 2 x 4 x 6 s_memtime stamps of sampled bf16 GEMM k-steps (VAP_GEMM2_STAMPS=1) */
-int vap_test_read_gemm_stamps(unsigned long long* out);
+int vap_test_read_gemm_stamps(unsigned long long* out);  /* + 8 x 6 tile-phase stamps after the 8 x 2 x 4 x 6 */
 /* timing diagnostics: 8 x 4 x 5 s_memtime stamps of bf16 LSTM steps 100..103 (VAP_LSTM_STAMPS=1) */
 int vap_test_read_lstm_stamps(unsigned long long* out);
 

@@ -34,9 +34,14 @@ def main():
         N.check(lib.vap_test_gemm(1, P(A), lda, rin * lda, P(W), K, Nn, None, M, S, P(C), Nn, M * Nn, None, Nn,
                                   M * Nn, None, None, 0, 0, 0, st))
     torch.cuda.synchronize()
-    buf = np.zeros((8, 2, 4, 6), dtype=np.uint64)
-    N.check(lib.vap_test_read_gemm_stamps(ctypes.c_void_p(buf.ctypes.data)))
-    b = buf.astype(np.int64)
+    allb = np.zeros(8 * 2 * 4 * 6 + 8 * 6, dtype=np.uint64)
+    N.check(lib.vap_test_read_gemm_stamps(ctypes.c_void_p(allb.ctypes.data)))
+    b = allb[:384].reshape(8, 2, 4, 6).astype(np.int64)
+    tb = allb[384:].reshape(8, 6).astype(np.int64)
+    print("tile phases (wave 0): [prologue DMA, k-loop, epilogue math, store issue, store drain | total]")
+    for wg in range(8):
+        t = tb[wg]
+        print(f"wg{wg * 64:4d}: " + " ".join(f"{t[k + 1] - t[k]:6d}" for k in range(5)) + f" | {t[5] - t[0]:6d}")
     names = ["dma+frag", "->bar", "bar->", "mfma", "vmwait", "bar"]
     for wg in range(8):
         for h in range(2):

@@ -36,6 +36,9 @@ VAP_DEV int swz(int row, int c) { return c ^ ((row >> 2) & 2); }
 // k-steps 8..11: [LOAD start, fragments in, after LOAD barrier, MFMAs done, DMA wait done, after
 // COMPUTE barrier] -> g_g2_stamps[wg][wave 0/4][4 k-steps][6]
 __device__ unsigned long long g_g2_stamps[8][2][4][6];
+// tile phases of the same sampled workgroups (wave 0): [0] start, [1] first stages landed, [2] k-loop
+// done, [3] epilogue math done, [4] stores issued, [5] stores complete
+__device__ unsigned long long g_g2_tile[8][6];
 
 template <typename TOut, bool ST = false>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
@@ -56,6 +59,15 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
       if (samp >= 0 && kt >= 8 && kt < 12) g_g2_stamps[samp][wave >> 2][kt - 8][k] = t;
     }
   };
+  unsigned long long tst[6] = {};
+  auto tstamp = [&](int k) {
+    if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
+      tst[k] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  tstamp(0);
 
   // DMA sources: a piece (one wave instruction, 1 KiB) = 16 rows x 64 B; wave w fills pieces 2w and
   // 2w+1 of each operand image; lane -> (row 16p + lane/4, physical chunk lane%4) holding logical
@@ -120,6 +132,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  tstamp(1);
   if (grp == 1) __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
     // ---- LOAD
@@ -164,6 +177,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  tstamp(2);
 
   // ---------------------------------------------------------------- epilogue
   // lane holds C[m = m0 + wm*128 + i*16 + fr][n = n0 + wn*64 + j*16 + fc*4 + r]
@@ -242,6 +256,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
         acc[j][i] = f32x4{lo[0], lo[1], hi[0], hi[1]};
       }
   }
+  tstamp(3);
   TOut* __restrict__ C = (TOut*)g.C;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -256,6 +271,13 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
       if (arow) v += *(const f32x4*)(arow + j * 16);
       store4(crow + j * 16, v[0], v[1], v[2], v[3]);
     }
+  }
+  if constexpr (ST) {
+    tstamp(4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tstamp(5);
+    if (samp >= 0 && wave == 0)
+      for (int k = 0; k < 6; ++k) g_g2_tile[samp][k] = tst[k];
   }
 }
 
@@ -280,7 +302,9 @@ hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
 
 // diagnostics: copy the gemm2 k-step stamps (8 x 2 x 4 x 6) to host memory
 hipError_t read_gemm2_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_g2_stamps), sizeof(g_g2_stamps), 0, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_g2_stamps), sizeof(g_g2_stamps), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(out + 8 * 2 * 4 * 6, HIP_SYMBOL(g_g2_tile), sizeof(g_g2_tile), 0, hipMemcpyDeviceToHost);
 }
 
 template hipError_t launch_gemm2<bf16>(const GemmArgs&, hipStream_t);
