@@ -57,7 +57,7 @@ struct vap_handle {
   double tc_edge = 0.0;             // time chunks: first / last chunk fraction of the frames (0: even split)
   // forward: front-end / back-end boundaries (cumulative frame fractions, VAP_TC_FE / VAP_TC_BE;
   // "" = the even time_chunks split for both)
-  std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.4, 0.7, 0.9};
+  std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.384, 0.768, 0.896};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
   bool heads_chunked = true;  // time-chunked back end: heads per chunk (VAP_HEADS_CHUNKED=0: once at the end)
   bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
