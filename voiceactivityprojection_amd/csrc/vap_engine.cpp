@@ -59,7 +59,8 @@ struct vap_handle {
   // "" = the even time_chunks split for both)
   std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.384, 0.768, 0.896};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
-  bool heads_chunked = true;  // time-chunked back end: heads per chunk (VAP_HEADS_CHUNKED=0: once at the end)
+  bool heads_chunked = false;  // VAP_HEADS_CHUNKED=1: heads per back-end chunk (shorter tail after the
+                               // recurrence, but small GEMMs: 0.41 vs 0.19 ms; the caller stream binds)
   bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
                              // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
   bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
