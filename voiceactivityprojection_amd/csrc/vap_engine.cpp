@@ -788,7 +788,8 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
 // Combinator (modules.py:434-449) + heads (model.py:257-261) of a clip range, from the final
 // residual stream X.  On `st`.
 template <typename T>
-int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logits, float* vadl, hipStream_t st) {
+int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logits, float* vadl, hipStream_t st,
+          bool raw_ready = false) {
   const int S = r.ns(), T_ = p.T;
   const int64_t t1 = (int64_t)T_ * D;
   float* X = (float*)(ws + p.X) + r.s0() * t1;
@@ -804,7 +805,7 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
   T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
   {
     Timed tm(h, VAP_K_HEADS, st);
-    HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
+    if (!raw_ready) HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
     // channel-0 rows are the even sequences: stride 2*T*D over the clips of the range
     GemmArgs ga = gargs(RAW, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, T_, r.nc, HC, D, t1);
     ga.norm = 2;
@@ -1184,13 +1185,16 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
       if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, bst))) return rc;
     for (int l = 0; l < h->dims.cross_layers; ++l, ++li) {
-      bf16* xb = hchunk && l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
+      // the last layer's block kernel also writes x as bf16 (RAW): the combinator's input, so the
+      // heads need no separate fp32 -> bf16 pass over x
+      const bool xb_ok = h->block_fused && h->ffn_fused;
+      bf16* xb = xb_ok && l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
       if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst, xb))) return rc;
     }
     if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bst))) return rc;
   }
   if (!(h->heads_chunked && h->block_fused && h->ffn_fused && h->dims.cross_layers > 0) &&
-      (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst)))
+      (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst, h->block_fused && h->ffn_fused)))
     return rc;
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
