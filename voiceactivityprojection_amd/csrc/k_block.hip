@@ -595,6 +595,13 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
     return hipGetLastError();
   }
   static const int npf = getenv("VAP_LNPROJ_NPF") ? atoi(getenv("VAP_LNPROJ_NPF")) : 2;
+  if (npf == 4) {  // 4 k-steps in flight still fits two workgroups per CU (<= 128 VGPRs)
+    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, 4>), grid, dim3(512), 0, st, g);
+    else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, 4>), grid, dim3(512), 0, st, g);
+    else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, false, 4>), grid, dim3(512), 0, st, g);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (npf == 8) {
     if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, 8>), grid, dim3(512), 0, st, g);
     else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, 8>), grid, dim3(512), 0, st, g);
