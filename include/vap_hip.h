@@ -123,8 +123,8 @@ int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, i
 /* hipGraph replay of steady-state pushes (bf16 carry-over streams; VAP_STREAM_GRAPH=0 disables): the
  * caller-stream part of a push is captured once per (gate-ring offset, window buffer, output
  * pointers) state and replayed; the recurrence launch stays eager on a side stream.  Reports the
- * graphs captured, the replays so far and the hand-off error word (1 if a flag wait timed out;
- * synchronous). */
+ * graphs captured, the replays so far and the handle's hand-off error word (1 if a flag wait timed
+ * out since the last check; synchronous, does not clear it). */
 int vap_stream_graphs(vap_stream* s, int* graphs, int64_t* replays, int* handoff_error);
 /* Window back to zeros; the next push recomputes every row. */
 int vap_stream_reset(vap_stream* s, void* stream);
@@ -154,6 +154,13 @@ int vap_probs(const float* logits, const float* vad_logits, int batch, int frame
  * vap/objective.py:10-11). */
 int vap_labels_loss(const float* logits, const float* va, int batch, int frames, const int* bin_frames, int n_bins,
                     float threshold, int64_t* labels, float* loss, void* stream);
+
+/* Wait for `stream` (the caller's stream of the last call on h) and report a hand-off failure of
+ * the calls since the last check: VAP_ERR_HIP when a bounded flag wait of the persistent LSTM
+ * recurrence or of a captured stream push timed out (~2 s; their outputs are then invalid).
+ * Without it such a failure is reported by the next vap_forward / vap_forward_mono / vap_encode /
+ * vap_stream_push on the handle (a host read of a mapped word, no device sync). */
+int vap_synchronize(vap_handle* h, void* stream);
 
 /* Timing hook: record HIP events around every launch of kernel class `cls` (0 = off). */
 int vap_timing(vap_handle* h, int cls);
@@ -205,6 +212,9 @@ int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* 
 /* the same with weights already packed (vap_test_pack_weight) */
 int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
                           const float* gamma, const float* beta, int cus, void* stream);
+/* workspace plan of a forward (diagnostics): byte offsets of X1..X4 (conv1..4 rows), GX (gate rows),
+ * H0 (LSTM h), X (residual stream), the total, then the per-sequence strides s1..s4, sh (elements) */
+int vap_test_plan(const vap_handle* h, int batch, int64_t n_samples, int64_t* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled fused-block workgroups (VAP_BLOCK_STAMPS=1) */

@@ -31,7 +31,8 @@ OUT_KEYS = ("vad", "p_now", "p_future", "probs", "H")
 
 def step_extraction(waveform, model, device="cpu", context_time=20, step_time=5, fold_batch=16, **_):
     """Long-audio extraction (run.py:23-131): context+step windows, first fold kept whole, every
-    later fold contributes its last step_frames, tail fold covers the remainder.
+    later fold contributes its last step_frames, tail fold covers the remainder; "loss" is the first
+    fold's, as in the reference.
 
     All folds are processed in batches of ``fold_batch`` clips per probs() call."""
     n_samples = waveform.shape[-1]
@@ -45,14 +46,17 @@ def step_extraction(waveform, model, device="cpu", context_time=20, step_time=5,
 
     B = waveform.shape[0]
     flat = folds.reshape(-1, 2, chunk_samples)  # (n_folds * B, 2, chunk)
-    parts = {k: [] for k in OUT_KEYS}
+    parts = {k: [] for k in OUT_KEYS + ("loss",)}
     for i in range(0, flat.shape[0], fold_batch * B):
         o = model.probs(flat[i: i + fold_batch * B].to(device))
-        for k in OUT_KEYS:
+        for k in parts:
             parts[k].append(o[k])
     allo = {k: torch.cat(v, 0).view(folds.shape[0], B, *v[0].shape[1:]) for k, v in parts.items()}
     out = {k: torch.cat([allo[k][0]] + [allo[k][f][:, -step_frames:] for f in range(1, folds.shape[0])], dim=1)
            for k in OUT_KEYS}
+    # the reference's `out` starts as the first fold's probs() dict and only the OUT_KEYS grow, so
+    # the first fold's "loss" (B, chunk_frames - horizon) stays in it and reaches the JSON (run.py:66)
+    out["loss"] = allo["loss"][0]
     processed = out["p_now"].shape[1]
     if expected_frames != processed:
         omitted = expected_frames - processed

@@ -1,0 +1,105 @@
+"""Robustness of the persistent LSTM hand-off (bf16 path) at and beyond its CU budget, and error
+reporting when a hand-off wait times out.
+
+The time-pipelined forward runs ONE persistent recurrence launch whose workgroups (16 sequences
+each, a whole CU: W_hh resident in LDS + registers) spin on ready flags that the caller stream's
+conv kernels publish.  A launch that took every CU would leave the producers nowhere to run, so the
+engine caps the persistent launch at half the CUs (VAP_LSTM_MAX_WG overrides) and runs a larger
+batch through the same schedule in slices that fit.  Outputs must not depend on the slicing: every
+clip stays bit-identical to the same clip run alone.
+"""
+import numpy as np
+import pytest
+import torch
+
+from voiceactivityprojection_amd.weights import synthetic_state_dict, synthetic_waveform
+
+pytestmark = pytest.mark.gpu
+
+BF16_TOL = {"p_now": 5e-2, "p_future": 5e-2, "vad": 3e-2}
+
+
+def _model(precision="bf16"):
+    from vap.model import VapGPT
+
+    m = VapGPT(precision=precision)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed=0).items()}, strict=True)
+    return m.to("cuda").eval()
+
+
+def _batch(B, n, seed):
+    return torch.from_numpy(np.stack([synthetic_waveform(seed + i, n) for i in range(B)])).cuda()
+
+
+def _same_as_alone(m, w, full, idx):
+    for i in idx:
+        one = m.probs(w[i:i + 1])
+        for k in full:
+            assert torch.equal(full[k][i:i + 1], one[k]), f"batch dependence in {k} (clip {i})"
+
+
+def test_batch_above_persistent_cap_small(monkeypatch):
+    """VAP_LSTM_MAX_WG=2 (32 sequences): a 20-clip batch (3 workgroups) runs as two slices of 10
+    clips and still matches every clip run alone."""
+    monkeypatch.setenv("VAP_LSTM_MAX_WG", "2")
+    m = _model()
+    w = _batch(20, 40960, 700)
+    full = m.probs(w)
+    m.synchronize()
+    _same_as_alone(m, w, full, (0, 7, 19))
+
+
+def test_batch_at_and_above_default_cap():
+    """Real sizes around the default cap (half of the CUs; 128 workgroups = 1024 stereo clips on a
+    256-CU MI355X): 1000 clips run the persistent launch on 125 CUs with the producers on the rest,
+    2100 clips (263 workgroups, more than the chip has CUs) run as three slices of 700.  No
+    hand-off may time out, and sampled clips equal the same clip alone.  2.5 s clips (T = 125)."""
+    m = _model()
+    n = 40000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for B in (1000, 2100):
+        w = (0.1 * torch.randn(B, 2, n, device="cuda", generator=g)).clamp_(-1, 1)
+        full = m.probs(w)
+        m.synchronize()  # raises if any ready-flag wait timed out
+        assert full["probs"].shape == (B, 125, 256)
+        _same_as_alone(m, w, full, (0, B // 2, B - 1))
+        for k in ("probs", "p_now", "p_future", "vad", "H", "loss"):
+            assert torch.isfinite(full[k]).all(), (B, k)
+        del w, full
+        torch.cuda.empty_cache()
+
+
+def test_handoff_timeout_is_reported(monkeypatch):
+    """A ready flag that never arrives (test hook VAP_TEST_DROP_READY) makes the recurrence's bounded
+    wait give up after ~2 s: synchronize() raises, and so does the next forward if not checked; the
+    word is cleared once reported."""
+    monkeypatch.setenv("VAP_TEST_DROP_READY", "1")
+    m = _model()
+    w = _batch(2, 80000, 50)  # 5 s: T = 250, several time chunks
+    m(w)
+    with pytest.raises(RuntimeError, match="timed out"):
+        m.synchronize()
+    m.synchronize()  # reported once, then clear
+    m(w)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        m(w)  # the previous call's failure surfaces here
+
+
+def test_stream_above_cap_recomputes(monkeypatch):
+    """A stream whose recurrence would exceed the cap runs full-recompute pushes (sliced forwards of
+    the window, no carry-over) and still equals a full forward of the rolled window."""
+    monkeypatch.setenv("VAP_LSTM_MAX_WG", "1")
+    m = _model()
+    B, window, hop = 12, 48000, 16000  # 24 sequences: 2 workgroups > 1
+    st = m.stream(B, context_time=window / 16000, hop_time=hop / 16000)
+    assert st.reused_rows == 0
+    audio = _batch(B, 2 * hop, 10)
+    win = torch.zeros(B, 2, window, device="cuda")
+    for k in range(2):
+        blk = audio[..., k * hop:(k + 1) * hop]
+        out = st.push(blk, full=True)
+        win = torch.cat([win[..., hop:], blk], dim=-1)
+        ref = m(win)
+        assert torch.equal(out["logits"], ref["logits"]), k
+    st.synchronize()

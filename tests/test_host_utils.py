@@ -46,9 +46,10 @@ def test_step_extraction_matches_per_fold_reference_loop():
         o = m.probs(w[..., -chunk:])
         for k in run.OUT_KEYS:
             exp[k] = torch.cat([exp[k], o[k][:, -om:]], 1)
-    for k in run.OUT_KEYS:
+    for k in run.OUT_KEYS + ("loss",):  # "loss" stays the first fold's (reference run.py:66)
         assert got[k].shape == exp[k].shape, k
         torch.testing.assert_close(got[k], exp[k], atol=1e-5, rtol=1e-5)  # CPU batch-size noise of the oracle
+    assert set(got) == set(exp)
     assert got["p_now"].shape[1] == expected_frames
 
 

@@ -288,19 +288,25 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
       while (sync.seq_end[rb] <= s_last) ++rb;
     }
     if (tid == 0) {
-      // the producer stream publishes ready[r] after the range's gate projection completed; a
-      // system-scope acquire also invalidates this CU's and XCD's caches for the gx reads below
-      // bounded: after ~2 s (100 MHz s_memrealtime) give up, flag the error word and run on, so a
+      // the producer stream publishes ready[r] after the range's gate projection completed (its
+      // kernel boundary wrote the rows back).  Poll RELAXED (L2-served sc1 loads), then ONE
+      // agent-scope acquire (invalidates this CU's L1; the vmcnt wait holds the barrier until it has
+      // completed).  Never poll with system-scope acquires: each one is a `buffer_inv sc0 sc1`, and
+      // ~100 workgroups issuing them back to back corrupted the outputs of the conv / GEMM kernels
+      // running beside them (rows of sequence 0 at batch >= 640 x 2.5 s).
+      // Bounded: after ~2 s (100 MHz s_memrealtime) give up, flag the error word and run on, so a
       // lost flag can never hang the device (done counters are still published below)
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (int r = ra; r <= rb; ++r)
-        while (__hip_atomic_load(sync.ready + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < sync.epoch) {
+        while (__hip_atomic_load(sync.ready + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
           __builtin_amdgcn_s_sleep(8);
           if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
             if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
         }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
   }
@@ -359,17 +365,23 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
       const int c0 = chunk;
       while (chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) ++chunk;
       if (tid == 0) {
+        // release: write this XCD's L2 back (the h rows of every wave, drained above), then the
+        // counters (the consumer stream's wait-value and kernels read memory)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (int c = c0; c < chunk; ++c)
-          __hip_atomic_fetch_add(sync.done + c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (chunk < sync.nr) {
+          __hip_atomic_fetch_add(sync.done + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (chunk < sync.nr) {  // relaxed poll + one agent acquire, as at the start
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < sync.epoch) {
+          while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
             __builtin_amdgcn_s_sleep(8);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
               if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               break;
             }
           }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
       }
       if (chunk < sync.nr) {
@@ -386,8 +398,11 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
   if (sync.ready && !sync.time_mode) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's h stores are complete
     __syncthreads();
-    if (tid == 0)  // release: the consumer stream's kernels (any XCD) see every h of these ranges
-      for (int r = ra; r <= rb; ++r) __hip_atomic_fetch_add(sync.done + r, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {  // release: the consumer stream's kernels (any XCD) see every h of these ranges
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = ra; r <= rb; ++r) __hip_atomic_fetch_add(sync.done + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -515,13 +515,16 @@ hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows
 // runs on, so a lost flag never hangs the device).
 // ------------------------------------------------------------------------------------------
 namespace {
+// (the data the flag covers was written by earlier kernels of the stream: their kernel boundary
+// wrote it back; the kernels after a wait start behind a boundary too, so neither side needs more
+// than agent scope -- and a poll must not be a system-scope acquire: see k_lstm.hip)
 __global__ void flag_set_kernel(unsigned* p, unsigned v) {
-  if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void wait_geq_kernel(const unsigned* p, unsigned v, unsigned* err) {
   if (threadIdx.x != 0) return;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
     __builtin_amdgcn_s_sleep(8);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz: 2 s
       if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

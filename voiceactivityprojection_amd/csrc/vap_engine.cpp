@@ -75,6 +75,13 @@ struct vap_handle {
   // persistent-LSTM hand-off (bf16): ready[MAXMB] then done[MAXMB] counters in device memory,
   // monotonic across calls (epoch / cumulative expectations kept here)
   unsigned* sync_mem = nullptr;
+  // hand-off error word (1 when a bounded flag wait timed out, so that call's outputs are invalid):
+  // host-mapped, so the host reads it without a device sync (vap_forward returns the error on the
+  // next call on the handle, vap_synchronize right away)
+  unsigned* err_host = nullptr;
+  unsigned* err_dev = nullptr;
+  int test_drop_ready = -1;  // VAP_TEST_DROP_READY=c (tests only): never publish ready[c] -> the wait times out
+  int lstm_max_wg = 0;  // VAP_LSTM_MAX_WG: persistent recurrence launches at most this many workgroups
   unsigned epoch = 0;
   unsigned done_expect[MAXMB] = {};
   bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
@@ -100,6 +107,10 @@ struct vap_handle {
         hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && wv) {
       if (hipMalloc(&sync_mem, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
       if (hipMemset(sync_mem, 0, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
+      if (hipHostMalloc((void**)&err_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&err_dev, err_host, 0) != hipSuccess)
+        return VAP_ERR_HIP;
+      *err_host = 0;
       wait_value = true;
     }
     streams_ready = true;
@@ -120,6 +131,7 @@ struct vap_handle {
   ~vap_handle() {
     if (streams_ready) {
       if (sync_mem) (void)hipFree(sync_mem);
+      if (err_host) (void)hipHostFree(err_host);
       for (auto& st : side) (void)hipStreamDestroy(st);
       for (int i = 0; i < MAXMB; ++i) {
         (void)hipEventDestroy(mb_ev[i]);
@@ -981,6 +993,27 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   return VAP_OK;
 }
 
+// compute units of the current device (persistent kernels size their grid to the CUs they may use)
+static int device_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// A persistent recurrence launch spins (bounded) on ready flags that kernels of the caller's stream
+// publish.  Each of its workgroups fills a whole CU (W_hh resident: 160 KB LDS + every register),
+// so the launch may take at most this many CUs, or the producers could find no CU to run on and
+// every flag wait would time out.  Above it the forward uses plain per-range recurrence launches,
+// which wait for nothing (the workgroups just queue).
+static int lstm_wg_cap(const vap_handle* h) {
+  return h->lstm_max_wg > 0 ? h->lstm_max_wg : std::max(1, device_cus() / 2);
+}
+static bool persistent_fits(const vap_handle* h, int S) { return (S + 15) / 16 <= lstm_wg_cap(h); }
+
 // VapGPT.forward pipelined ALONG TIME (bf16, 1-layer LSTM).  The frames are cut into `nch` chunks;
 // on the caller's stream the front end of chunk c computes only the conv / gate-projection rows
 // that chunk needs (receptive fields: conv4 rows [., e) need conv3 rows < 2e+1, and so on down to
@@ -1091,19 +1124,23 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
   sy.gx_off = gx_off;
   sy.ready = h->sync_mem;
   sy.done = h->sync_mem + vap_handle::MAXMB;
-  sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
+  sy.error = h->err_dev;
   sy.epoch = ++h->epoch;
   sy.nr = t.nch;
   sy.time_mode = 1;
   for (int c = 0; c < t.nch; ++c) sy.seq_end[c] = t.seq_end[c];
-  const int nwg = (p.S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
-  for (int c = 0; c < t.nch; ++c) h->done_expect[c] += nwg;
   hipStream_t side = h->side[0];
   hipEvent_t fork = h->next_fork_event();
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
-  Timed tm(h, VAP_K_LSTM_REC, side);
-  HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, true));
+  {
+    Timed tm(h, VAP_K_LSTM_REC, side);
+    HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, true));
+  }
+  // the back ends wait for these counts: raise them only once the launch is in the queue (a failed
+  // launch must not leave later forwards waiting for arrivals that never come)
+  const int nwg = (p.S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
+  for (int c = 0; c < t.nch; ++c) h->done_expect[c] += nwg;
   return VAP_OK;
 }
 
@@ -1206,16 +1243,6 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
   return VAP_OK;
 }
 
-// compute units of the current device (persistent kernels size their grid to the CUs they may use)
-static int device_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
 
 // bf16 CPC rows of conv4 range [a4, b4) of every sequence, with the conv1..conv3 rows they need
 // (k4 s2 p1 layers: rows [a, b) need input rows [2a-1, 2b+1) clipped to the layer; conv1 rows come
@@ -1287,7 +1314,9 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
     if (!t.fe_pub[c]) continue;
     if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st))) return rc;
     done_rows = t.seq_end[c];
-    for (; published <= c; ++published) HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published), sy.epoch, 0));
+    for (; published <= c; ++published)
+      if (published != h->test_drop_ready)
+        HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published), sy.epoch, 0));
   }
   return tc_back_end(h, p, t, sy, ws, logits, vadl, st);
 }
@@ -1303,6 +1332,25 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   const Plan p = plan_for(h, B, N);
   const int S = p.S;
   const int64_t* L = p.L;
+  if constexpr (sizeof(T) == 2) {
+    // A batch whose recurrence would not fit the persistent launch's CU budget runs the same
+    // time-pipelined schedule slice by slice (identical kernels, so identical outputs per clip).
+    if (h->use_time_chunks() && !enc_out && p.QKVL && !h->amap_active() && !persistent_fits(h, S)) {
+      int rc;
+      if ((rc = h->ensure_streams())) return rc;
+      if (h->wait_value) {
+        const int per = std::max(1, lstm_wg_cap(h) * 16 / 2);  // clips per slice (2 sequences each)
+        const int ns = (B + per - 1) / per;
+        for (int i = 0; i < ns; ++i) {
+          const int c0 = (int)((int64_t)B * i / ns), c1 = (int)((int64_t)B * (i + 1) / ns);
+          if ((rc = run_forward<T>(h, wav + (int64_t)c0 * 2 * N, c1 - c0, N, logits + (int64_t)c0 * p.T * 256,
+                                   vadl + (int64_t)c0 * p.T * 2, ws, st)))
+            return rc;
+        }
+        return VAP_OK;
+      }
+    }
+  }
   // pad rows (conv zero padding lives in explicit rows)
   if constexpr (sizeof(T) == 4) {  // bf16 mode never materialises conv0
     T* X0 = (T*)(ws + p.X0);
@@ -1329,7 +1377,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   }
   int rc;
   if constexpr (sizeof(T) == 2) {
-    if (h->use_time_chunks() && !enc_out && p.QKVL && !h->amap_active()) {
+    if (h->use_time_chunks() && !enc_out && p.QKVL && !h->amap_active() && persistent_fits(h, S)) {
       if ((rc = h->ensure_streams())) return rc;
       if (h->wait_value) return run_forward_tc(h, p, wav, N, logits, vadl, ws, st);
     }
@@ -1342,7 +1390,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   }
   if ((rc = h->ensure_streams())) return rc;
   if constexpr (sizeof(T) == 2) {
-    if (h->wait_value && h->persistent_lstm) {
+    if (h->wait_value && h->persistent_lstm && persistent_fits(h, S)) {
       // One persistent LSTM launch on a side stream covers every range: its workgroups start as
       // each range's gate projection lands (ready flag written by this stream) and publish done
       // counters the back ends wait on.  No per-range launches, so no range queues behind another
@@ -1351,17 +1399,18 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       LstmSync sy{};
       sy.ready = h->sync_mem;
       sy.done = h->sync_mem + vap_handle::MAXMB;
-      sy.error = h->sync_mem + 2 * vap_handle::MAXMB;
+      sy.error = h->err_dev;
       sy.epoch = ++h->epoch;
       sy.nr = nr;
       for (int i = 0; i < nr; ++i) sy.seq_end[i] = 2 * (rs[i].c0 + rs[i].nc);
+      unsigned add[vap_handle::MAXMB] = {};
       for (int wg = 0; wg * 16 < S; ++wg) {  // done increments per range (launch_lstm_resident: 16 sequences per WG)
         const int s_first = wg * 16, s_last = std::min(S, s_first + 16) - 1;
         int ra = 0;
         while (sy.seq_end[ra] <= s_first) ++ra;
         int rb = ra;
         while (sy.seq_end[rb] <= s_last) ++rb;
-        for (int r = ra; r <= rb; ++r) ++h->done_expect[r];
+        for (int r = ra; r <= rb; ++r) ++add[r];
       }
       hipStream_t side = h->side[0];
       hipEvent_t fork = h->next_fork_event();
@@ -1372,6 +1421,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
         HIPCHK(launch_lstm_resident((const bf16*)(ws + p.GX), S, (int)L[4], (const bf16*)h->W<T>("whh_l0"),
                                     (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh, side, &sy, true));
       }
+      for (int i = 0; i < nr; ++i) h->done_expect[i] += add[i];  // only after a successful launch
       for (int i = 0; i < nr; ++i) {
         if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
         if ((rc = lstm_layer<T>(h, p, ws, 0, rs[i], st, st, false))) return rc;
@@ -1519,7 +1569,7 @@ int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, floa
   sy.gx_off = (int)off;
   sy.ready = s->gsync;
   sy.done = s->gsync + vap_handle::MAXMB;
-  sy.error = s->gsync + 2 * vap_handle::MAXMB;
+  sy.error = h->err_dev;
   sy.epoch = 1;
   sy.nr = t.nch;
   sy.time_mode = 1;
@@ -1637,6 +1687,16 @@ int stream_zero(vap_stream* s, hipStream_t st) {
 }  // namespace
 
 
+// A bounded hand-off wait of an earlier call on this handle timed out (its outputs are invalid):
+// report it once and clear the word.  Reads host-mapped memory, no device sync.
+static int take_handoff_error(vap_handle* h) {
+  if (!h->err_host || __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) == 0) return VAP_OK;
+  __atomic_store_n(h->err_host, 0u, __ATOMIC_RELEASE);
+  return fail(VAP_ERR_HIP,
+              "a persistent LSTM / stream hand-off wait timed out (~2 s) in an earlier call on this handle: "
+              "that call's outputs are invalid");
+}
+
 // ============================================================================== C ABI
 extern "C" {
 
@@ -1672,6 +1732,8 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
+  if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
+  if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;
@@ -1777,6 +1839,7 @@ int vap_forward(vap_handle* h, const float* waveform, int batch, int64_t n_sampl
   if (h->dims.mono) return fail(VAP_ERR_INVALID, "mono handle: use vap_forward_mono");
   if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
   if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  if (int rc = take_handoff_error(h)) return rc;
   size_t need = 0;
   int rc = vap_workspace_size(h, batch, n_samples, &need);
   if (rc) return rc;
@@ -1806,6 +1869,7 @@ int vap_forward_mono(vap_handle* h, const float* waveform, const float* va, cons
   if (!h->dims.mono) return fail(VAP_ERR_INVALID, "vap_forward_mono needs a handle created with dims.mono = 1");
   if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
   if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  if (int rc = take_handoff_error(h)) return rc;
   size_t need = 0;
   int rc = vap_workspace_size(h, batch, n_samples, &need);
   if (rc) return rc;
@@ -1864,7 +1928,8 @@ int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t 
   // carry-over is exact only for hops of whole conv4 rows (160 samples) on the time-chunked bf16 path
   const bool bf = h->dims.precision == VAP_PRECISION_BF16;
   if (bf && h->use_time_chunks() && h->ensure_streams()) return bail("streams");  // sets wait_value
-  s->reuse = bf && h->use_time_chunks() && h->wait_value && hop_samples % 160 == 0;
+  // (the carry-over push needs the persistent recurrence launch: within its CU cap)
+  s->reuse = bf && h->use_time_chunks() && h->wait_value && hop_samples % 160 == 0 && persistent_fits(h, S);
   if (const char* e = getenv("VAP_STREAM_REUSE")) s->reuse = s->reuse && atoi(e) != 0;  // A/B: 0 = recompute
   if (s->reuse) {
     if (hipMalloc(&s->gx, (size_t)S * L[4] * 4 * D * sizeof(bf16)) != hipSuccess) return bail("gate buffer");
@@ -1900,7 +1965,14 @@ int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t 
 
 int vap_stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad_logits, void* stream) {
   if (!s || !hop_audio || !logits || !vad_logits) return fail(VAP_ERR_INVALID, "null argument");
+  if (int rc = take_handoff_error(s->h)) return rc;
   return stream_push(s, hop_audio, logits, vad_logits, (hipStream_t)stream);
+}
+
+int vap_synchronize(vap_handle* h, void* stream) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return take_handoff_error(h);
 }
 
 int vap_stream_info(const vap_stream* s, int* frames, int64_t* window_samples, int64_t* hop_samples,
@@ -1920,7 +1992,10 @@ int vap_stream_graphs(vap_stream* s, int* graphs, int64_t* replays, int* handoff
   if (replays) *replays = s->graph_replays;
   if (handoff_error) {
     unsigned e = 0;
-    if (s->gsync) HIPCHK(hipMemcpy(&e, s->gsync + 2 * vap_handle::MAXMB, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (s->h->err_host) {
+      HIPCHK(hipDeviceSynchronize());
+      e = __atomic_load_n(s->h->err_host, __ATOMIC_ACQUIRE);
+    }
     *handoff_error = (int)e;
   }
   return VAP_OK;
@@ -1938,6 +2013,7 @@ int vap_encode(vap_handle* h, const float* waveform, int batch, int64_t n_sample
   if (!h || !waveform || !out || !workspace) return fail(VAP_ERR_INVALID, "null argument");
   if (!h->finalized) return fail(VAP_ERR_WEIGHTS, "vap_finalize not called after loading parameters");
   if (batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad batch / n_samples");
+  if (int rc = take_handoff_error(h)) return rc;
   size_t need = 0;
   int rc = vap_workspace_size(h, batch, n_samples, &need);
   if (rc) return rc;
@@ -1986,6 +2062,16 @@ int vap_labels_loss(const float* logits, const float* va, int batch, int frames,
     return fail(VAP_ERR_TOO_SHORT, "maximum size for tensor at dimension 1 is " + std::to_string(frames - 1) +
                                        " but size is " + std::to_string(horizon));
   HIPCHK(launch_labels_loss(logits, va, batch, frames, bin_frames, n_bins, threshold, labels, loss, (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_test_plan(const vap_handle* h, int batch, int64_t n_samples, int64_t* out) {
+  if (!h || !out || batch <= 0 || n_samples <= 0) return fail(VAP_ERR_INVALID, "bad argument");
+  const Plan p = plan_for(h, batch, n_samples);
+  const size_t v[] = {p.X1, p.X2, p.X3, p.X4, p.GX, p.H0, p.X, p.total};
+  const int64_t st[] = {p.s1, p.s2, p.s3, p.s4, p.sh};
+  for (int i = 0; i < 8; ++i) out[i] = (int64_t)v[i];
+  for (int i = 0; i < 5; ++i) out[8 + i] = st[i];
   return VAP_OK;
 }
 

@@ -16,6 +16,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .utils import frame_lengths
+
 COMPACT_KEYS = ("p_now", "p_future", "vad", "H")
 
 
@@ -57,9 +59,26 @@ def gather_outputs(out: Dict[str, torch.Tensor], keys: Sequence[str] = COMPACT_K
     return res if rank == dst else None
 
 
+def empty_probs(n_samples: int, device, n_classes: int = 256, horizon_frames: int = 100) -> Dict[str, torch.Tensor]:
+    """Zero-clip ``probs()`` outputs for ``n_samples`` per channel: the shapes a 0-row batch would have
+    (probs (0, T, 256), vad / p_now / p_future (0, T, 2), H (0, T), loss (0, T - horizon))."""
+    T = frame_lengths(n_samples)[-1]
+    z = lambda *shape: torch.zeros(shape, dtype=torch.float32, device=device)  # noqa: E731
+    return {"probs": z(0, T, n_classes), "vad": z(0, T, 2), "p_now": z(0, T, 2), "p_future": z(0, T, 2),
+            "H": z(0, T), "loss": z(0, max(T - horizon_frames, 0))}
+
+
 def probs_sharded(model, waveform_global: torch.Tensor, rank: int, world: int, device,
                   keys: Sequence[str] = COMPACT_KEYS, group=None):
-    """Run ``model.probs`` on this rank's slice of a global batch and gather to rank 0."""
+    """Run ``model.probs`` on this rank's slice of a global batch and gather to rank 0.
+
+    A rank whose slice is empty (global batch < world) skips the engine (which rejects a batch of
+    0) and still joins the gather with zero-row outputs of the right trailing shapes, so no rank is
+    left waiting in the collective."""
     s, e = shard_range(waveform_global.shape[0], rank, world)
-    out = model.probs(waveform_global[s:e].to(device))
+    if e > s:
+        out = model.probs(waveform_global[s:e].to(device))
+    else:
+        out = empty_probs(waveform_global.shape[-1], device, model.objective.n_classes,
+                          int(round(model.horizon_time * model.frame_hz)))
     return gather_outputs(out, keys, dst=0, group=group)

@@ -46,6 +46,9 @@ def load_older_state_dict(path="example/VAP_3mmz3t0u_50Hz_ad20s_134-epoch9-val_2
     return new_sd
 
 
+_SYNC_CHECK = os.environ.get("VAP_SYNC_CHECK", "0") not in ("", "0")
+
+
 @dataclass
 class VapConfig:
     sample_rate: int = 16_000
@@ -274,7 +277,19 @@ class VapGPT(nn.Module):
         vad = torch.empty(B, T, 2, device=waveform.device, dtype=torch.float32)
         N.check(N.lib().vap_forward(h, waveform.data_ptr(), B, n, logits.data_ptr(), vad.data_ptr(), ws.data_ptr(),
                                     ws.numel(), N.stream_ptr(waveform.device)), "vap_forward")
+        if _SYNC_CHECK:
+            self.synchronize(waveform.device)
         return {"logits": logits, "vad": vad}
+
+    def synchronize(self, device=None) -> None:
+        """Wait for the engine's work on the current stream and raise if a hand-off of the persistent
+        LSTM recurrence timed out since the last check (its outputs would be invalid).  Without this
+        call such a failure raises from the next forward on the model.  ``VAP_SYNC_CHECK=1`` runs it
+        after every forward (debugging: it costs a device sync per call)."""
+        if self._handle is None:
+            return
+        dev = device if device is not None else self._handle_key[0]
+        N.check(N.lib().vap_synchronize(self._handle, N.stream_ptr(dev)), "vap_synchronize")
 
     def _forward_attention(self, waveform: Tensor) -> Dict[str, Tensor]:
         waveform = self._check_input(waveform)

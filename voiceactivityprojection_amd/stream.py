@@ -69,6 +69,12 @@ class VapStream:
                 "vap_stream_graphs")
         return {"graphs": g.value, "replays": r.value, "handoff_error": e.value}
 
+    def synchronize(self):
+        """Wait for the pushes so far and raise if one of their hand-off waits timed out
+        (otherwise reported by the next push)."""
+        self._check_handle()
+        N.check(N.lib().vap_synchronize(self._h, N.stream_ptr(self.device)), "vap_synchronize")
+
     def _check_handle(self):
         if self._s is None:
             raise RuntimeError("stream closed")

@@ -15,6 +15,21 @@ from torch import Tensor
 VAD_LIST = List[List[List[float]]]
 
 
+def frame_lengths(n_samples: int) -> List[int]:
+    """Output lengths of conv0..conv4 and the 50 Hz frame count T for ``n_samples`` per channel
+    (host arithmetic, no device): the CPC conv specs (k, s, p) = (10, 5, 3), (8, 4, 2), (4, 2, 1) x 3
+    (vap/encoder_components.py:83-92) and the causal downsample k5 s2, left pad 4
+    (vap/encoder.py:24-31, CConv1d vap/encoder_components.py:454-460).  Same chain as the engine's
+    vap_frame_lengths."""
+    lens = []
+    n = int(n_samples)
+    for k, st, pd in ((10, 5, 3), (8, 4, 2), (4, 2, 1), (4, 2, 1), (4, 2, 1)):
+        n = (n + 2 * pd - k) // st + 1 if n + 2 * pd >= k else 0
+        lens.append(n)
+    lens.append((n + 4 - 5) // 2 + 1 if n > 0 else 0)
+    return lens
+
+
 def time_to_frames(t: float, hop_time: float) -> int:
     """vap/audio.py:19-20."""
     return int(t / hop_time)
