@@ -135,22 +135,25 @@ def test_attention(prec, kv_swap):
     assert err <= tol, f"{prec}: attention max err {err}"
 
 
-@pytest.mark.parametrize("prec,variant", [("fp32", 0), ("bf16", 0), ("bf16", 1), ("bf16", 2)])
-def test_lstm(prec, variant):
+@pytest.mark.parametrize("prec,variant,S", [("fp32", 0, 20), ("bf16", 0, 20), ("bf16", 1, 20), ("bf16", 2, 20),
+                                            ("bf16", 3, 20), ("bf16", 3, 300)])
+def test_lstm(prec, variant, S):
     """variant 0 = the resident kernel for that precision (bf16: W_hh resident in AGPR/VGPR/LDS,
-    bf16 gx); variant 1 = the L2-streaming kernel in bf16 (fp32 gx); variant 2 = the engine's bf16
-    path: gate scales folded into W_hh and gx (the ABI scales gx), exp2-domain cell."""
+    bf16 gx); variant 1 = the L2-streaming kernel in bf16 (fp32 gx); variant 2 = the resident bf16
+    path with gate scales folded into W_hh and gx (the ABI scales gx), exp2-domain cell; variant 3 =
+    the engine's default: W_hh split over workgroup pairs that exchange h halves every step (S = 300:
+    19 pairs, a padding pair in the last 16-block group)."""
     N = lib()
     code, dt = PREC[prec]
     g = torch.Generator().manual_seed(3)
-    S, T = 20, 37
+    T = 37
     gx = torch.randn(S, T, 1024, generator=g)
-    if prec == "bf16" and variant in (0, 2):
+    if prec == "bf16" and variant in (0, 2, 3):
         gx = gx.to(torch.bfloat16).float()
     whh = (torch.rand(1024, 256, generator=g) * 2 - 1) / 16
     out = torch.zeros(S, T, 256, device="cuda", dtype=dt)
     packed = torch.zeros(1024 * 256, device="cuda", dtype=dt)
-    gxd = gx.cuda().to(torch.bfloat16) if (prec == "bf16" and variant in (0, 2)) else gx.cuda()
+    gxd = gx.cuda().to(torch.bfloat16) if (prec == "bf16" and variant in (0, 2, 3)) else gx.cuda()
     whd = whh.cuda()
     _run(N.lib().vap_test_lstm, code, _p(gxd), S, T, _p(whd), _p(packed), _p(out), variant, _st())
     wr = whh.to(dt).float()

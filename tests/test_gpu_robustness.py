@@ -39,8 +39,8 @@ def _same_as_alone(m, w, full, idx):
 
 
 def test_batch_above_persistent_cap_small(monkeypatch):
-    """VAP_LSTM_MAX_WG=2 (32 sequences): a 20-clip batch (3 workgroups) runs as two slices of 10
-    clips and still matches every clip run alone."""
+    """VAP_LSTM_MAX_WG=2: one pair of workgroups (16 sequences) per persistent launch, so a 20-clip
+    batch runs as three slices and still matches every clip run alone."""
     monkeypatch.setenv("VAP_LSTM_MAX_WG", "2")
     m = _model()
     w = _batch(20, 40960, 700)
@@ -50,14 +50,14 @@ def test_batch_above_persistent_cap_small(monkeypatch):
 
 
 def test_batch_at_and_above_default_cap():
-    """Real sizes around the default cap (half of the CUs; 128 workgroups = 1024 stereo clips on a
-    256-CU MI355X): 1000 clips run the persistent launch on 125 CUs with the producers on the rest,
-    2100 clips (263 workgroups, more than the chip has CUs) run as three slices of 700.  No
-    hand-off may time out, and sampled clips equal the same clip alone.  2.5 s clips (T = 125)."""
+    """Real sizes around the default cap (half of the CUs: 128 workgroups = 64 pairs = 512 stereo
+    clips on a 256-CU MI355X): 500 clips run one persistent launch on 126 CUs with the producers on
+    the rest, 1000 and 2100 clips (more recurrence workgroups than the chip has CUs) run as slices.
+    No hand-off may time out, and sampled clips equal the same clip alone.  2.5 s clips (T = 125)."""
     m = _model()
     n = 40000
     g = torch.Generator(device="cuda").manual_seed(5)
-    for B in (1000, 2100):
+    for B in (500, 1000, 2100):
         w = (0.1 * torch.randn(B, 2, n, device="cuda", generator=g)).clamp_(-1, 1)
         full = m.probs(w)
         m.synchronize()  # raises if any ready-flag wait timed out

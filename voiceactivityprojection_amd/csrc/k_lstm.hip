@@ -9,6 +9,7 @@
 // h_{t-1} is exchanged through a padded LDS image (one barrier per step); W_hh is pre-packed in
 // MFMA-fragment order so every wave-load is one contiguous KiB.
 #include <cstdlib>
+#include <type_traits>
 
 #include "vap_common.h"
 #include "vap_kernels.h"
@@ -406,6 +407,266 @@ __global__ __launch_bounds__(256, 1) void lstm_resident_kernel(const bf16* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// W_hh split over a PAIR of workgroups: two CUs per 16 sequences.
+//
+// The single-CU kernel above is issue-bound on one SIMD: per step each wave issues 128 MFMAs and 16
+// cells (10 transcendentals each) per lane with no second wave to hide latency (~3.4 us per step
+// beside the other kernels, 2000 dependent steps per 20 s clip: the recurrence is the critical
+// chain of the time-pipelined forward).  Here workgroup half p of a pair owns hidden units
+// [128p, 128p + 128): 4 gates x 128 units = 512 W_hh rows = 256 KiB bf16, held entirely in registers
+// by 8 waves (2 per SIMD, 32 fragments each); wave w owns units 128p + 16w .. +16 (one row tile per
+// gate, 32 MFMAs and 4 cells per lane per step).  Each step needs the partner's half of h_{t-1}:
+//   * every lane publishes its 4 h values (units 128p + 16w + 4(lane>>4) + r, sequence lane&15) as
+//     two 8-byte {2 x bf16, tag} granules in ONE 16-byte write-through (sc1) store into the pair's
+//     exchange slot for step parity t&1; tag = (launch epoch, step);
+//   * the same lane of the partner polls that 16-byte slot with sc1 loads until both tags match
+//     (no separate flag: the data carries its own readiness; a granule is never torn), then writes
+//     the 4 values into its LDS image of h;
+//   * the poll is issued before this half's own-unit k-steps (half of the MFMAs), so most of the
+//     exchange latency overlaps them; one barrier publishes the partner's half, a second the own h_t.
+// Two parity slots suffice: a half can write h_t only after reading the partner's h_{t-1}, which the
+// partner published only after reading our h_{t-2} (the slot being overwritten).
+// Pairs are blocks (b, b+8) of each 16-block group (same XCD under round-robin placement: speed
+// only); every spin is bounded (~2 s, then the error word is set and the step runs on).
+// ------------------------------------------------------------------------------------------
+constexpr int P_NW = 8, P_NF = 32;  // waves per workgroup, W fragments per wave (4 gates x 8 k-steps)
+constexpr int P_SLOT = 2 * 2 * 512;  // 16-byte exchange slots per pair: [half][parity][lane of the workgroup]
+
+VAP_DEV u32x4 xload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);  // sc1: L2-coherent, bypasses L1
+}
+
+template <bool PRE, bool ST>
+__global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restrict__ gx, int S, int Tn,
+                                                          const chunk16* __restrict__ wp, bf16* __restrict__ out,
+                                                          int64_t out_seq_stride, LstmSync sync, u32x4* xbuf) {
+  __shared__ __attribute__((aligned(16))) unsigned char hb[NS * 512];  // h_{t-1} [seq][256], chunk ^= seq
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int grp = (b >> 4) * 8 + (b & 7), p = (b >> 3) & 1;
+  if (grp * NS >= S) return;  // padding pair (both halves leave)
+  const int sl = lane & 15;
+  const int seq = grp * NS + sl;
+  const bool valid = seq < S;
+  const int u0 = 128 * p + 16 * w + 4 * (lane >> 4);  // this lane's 4 units (rows of the gate tiles)
+
+  chunk16 wa[P_NF];  // fragment f = g*8 + kk: rows g*256 + 128p + 16w + (lane&15), k = 32kk + 8(lane>>4) + e
+  const chunk16* wsrc = wp + (int64_t)(p * P_NW + w) * P_NF * 64 + lane;
+#pragma unroll
+  for (int f = 0; f < P_NF; ++f) wa[f] = wsrc[f * 64];
+  for (int i = tid; i < NS * 512 / 4; i += 512) ((unsigned*)hb)[i] = 0u;  // h_{-1} = 0 (both halves)
+
+  // exchange slots of this pair: ours [p][parity], the partner's [1-p][parity]; lane tid <-> lane tid
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xbuf + (int64_t)grp * P_SLOT, (uint32_t)(P_SLOT * 16));
+  const uint32_t x_own = (uint32_t)(((p * 2) * 512 + tid) * 16), x_rem = (uint32_t)((((1 - p) * 2) * 512 + tid) * 16);
+  const uint32_t tag_base = sync.xepoch * (uint32_t)(Tn + 1) + 1u;  // tag of step t: tag_base + t (never 0)
+
+  int ra = 0, rb = -1;
+  if (sync.ready) {
+    if (sync.time_mode) {
+      rb = 0;
+    } else {
+      const int s_first = grp * NS, s_last = min(S, s_first + NS) - 1;
+      while (sync.seq_end[ra] <= s_first) ++ra;
+      rb = ra;
+      while (sync.seq_end[rb] <= s_last) ++rb;
+    }
+    if (tid == 0) {  // relaxed poll + one agent acquire (see lstm_resident_kernel)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (int r = ra; r <= rb; ++r)
+        while (__hip_atomic_load(sync.ready + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
+          __builtin_amdgcn_s_sleep(8);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + u0;
+  const int goff = sync.gx_off;
+  auto grow = [&](int t) -> int64_t {
+    const int r = t + goff;
+    return (int64_t)(r >= Tn ? r - Tn : r) * G4;
+  };
+  bf16x4 gn[4];
+  __syncthreads();  // hb zeroed; ready acquired
+#pragma unroll
+  for (int g = 0; g < 4; ++g) gn[g] = *(const bf16x4*)(gxs + grow(0) + g * HD);
+
+  auto hfrag = [&](int kk) -> chunk16 {  // B operand: h[32kk + 8(lane>>4) + e][seq lane&15]
+    return *(const chunk16*)(hb + sl * 512 + (((kk * 4 + (lane >> 4)) ^ sl) << 4));
+  };
+  auto hput = [&](int u, u32x2 v) {  // 4 consecutive units (u % 4 == 0) of sequence sl
+    *(u32x2*)(hb + sl * 512 + (((u >> 3) ^ sl) << 4) + (u & 7) * 2) = v;
+  };
+  const bool samp = ST && blockIdx.x < 8 && tid == 0;
+  __shared__ unsigned long long stl[ST ? 20 : 1];  // stamps go to LDS (a global store would join the counted vmcnt)
+  auto stamp = [&](int t, int k) {  // diagnostics: g_lstm_stamps[wg][step 100..103][point]
+    if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long v = __builtin_amdgcn_s_memtime();
+      if (samp && t >= 100 && t < 104) stl[(t - 100) * 5 + k] = v;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int chunk = 0;
+  bool dead = false;  // an exchange wait timed out (error word set): the remaining steps do not wait
+  // the own / partner k-step ranges index the fragment array: compile-time per half, so the fragments
+  // stay in registers (a runtime index would put them in scratch)
+  // Every vector-memory op of the step loop is issued by inline asm in a fixed order, and the waits
+  // are counted by hand: vmcnt retires in issue order, and the compiler's own accounting falls back to
+  // vmcnt(0) at the loop's merge points, which would make each exchange wait also wait for the gx
+  // prefetch just issued.  Per step t (steady state):
+  //   P  exchange poll (partner's h_{t-1}, t > 0) | G  gx rows of step t+2 (4 loads) | R  poll retries
+  //   X  exchange publish (h_t)                   | O  h_t row store
+  // -> the poll wait is vmcnt(4) (G may stay in flight); gx of step t (issued in step t-2) is waited
+  // with vmcnt(9) (at least R X O + P G R X O are younger).  Retries only add younger ops, so both
+  // waits stay sufficient.
+  const __amdgpu_buffer_rsrc_t orsc =
+      make_rsrc(out + (int64_t)grp * NS * out_seq_stride, (uint32_t)((int64_t)min(NS, S - grp * NS) * out_seq_stride * 2));
+  const uint32_t o_lane = (uint32_t)(((int64_t)sl * out_seq_stride + u0) * 2);  // lanes of missing sequences: out of range
+  auto gload = [&](u32x2 (&gv)[4], int row) {
+    const bf16* a = gxs + grow(row);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(gv[g]) : "v"(a + g * HD) : "memory");
+  };
+  u32x2 ga[4], gb[4];  // gx ring: ga for even steps, gb for odd
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    ga[g] = __builtin_bit_cast(u32x2, gn[g]);
+    gb[g] = *(const u32x2*)(gxs + grow(Tn > 1 ? 1 : 0) + g * HD);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto run = [&](auto half) {
+  constexpr int kown = 4 * decltype(half)::value, krem = 4 - kown;
+  auto step = [&](const int t, u32x2 (&gc)[4], u32x2 (&go)[4]) {
+    stamp(t, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t >= 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // gc (gx of step t) landed
+    stamp(t, 1);
+    f32x4 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const bf16x4 v = __builtin_bit_cast(bf16x4, gc[g]);
+      acc[g] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    }
+    // the partner's h_{t-1}: issue the poll now, consume it after the own-unit k-steps
+    const uint32_t xo_rem = x_rem + (uint32_t)(((t - 1) & 1) * 512 * 16);
+    u32x4 xv = {0u, 0u, 0u, 0u};
+    if (t > 0) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(xv) : "v"(xo_rem), "s"(xr) : "memory");
+    gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const chunk16 hf = hfrag(kown + q);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = mfma_chunk<bf16>(wa[g * 8 + kown + q], hf, acc[g]);
+    }
+    stamp(t, 2);
+    if (t > 0) {
+      __builtin_amdgcn_sched_barrier(0);  // the own-unit MFMAs stay ahead of the wait
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // P landed (G may still be in flight)
+      const uint32_t want = tag_base + (uint32_t)(t - 1);
+      uint64_t t0 = 0;
+      while (!dead && !sync.xnowait && !__all(xv[1] == want && xv[3] == want)) {
+        if (!t0) {
+          t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+          if (sync.error && lane == 0) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          dead = true;  // the partner is gone: no further waits (the launch drains in microseconds)
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_waitcnt vmcnt(0)" : "=v"(xv) : "v"(xo_rem), "s"(xr)
+                     : "memory");
+      }
+      hput(u0 ^ 128, u32x2{xv[0], xv[2]});  // the partner lane's units: 128(1-p) + 16w + 4(lane>>4)
+    }
+    stamp(t, 3);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // B1: the partner's half of h_{t-1} is in the image
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const chunk16 hf = hfrag(krem + q);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = mfma_chunk<bf16>(wa[g * 8 + krem + q], hf, acc[g]);
+    }
+    float hv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lstm_cell<PRE>(acc, r, c[r], hv[r]);
+    const u32x2 hp = pack_bf16x4(hv[0], hv[1], hv[2], hv[3]);
+    const uint32_t tag = tag_base + (uint32_t)t;
+    const u32x4 xo = {hp[0], tag, hp[1], tag};
+    const uint32_t xoff = x_own + (uint32_t)((t & 1) * 512 * 16);
+    if (sync.xplain)  // experiment: stays in the XCD's L2
+      asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(xo), "v"(xoff), "s"(xr) : "memory");
+    else  // publish to the partner (write-through)
+      asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 2" ::"v"(xo), "v"(xoff), "s"(xr) : "memory");
+    // (the s_nops: a VALU write of a store's data VGPRs right after a dwordx3/x4 store is a hazard the
+    // compiler does not see through inline asm)
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
+                 "s"(orsc) : "memory");
+    hput(u0, hp);  // own units of h_t (the own-unit reads of this step retired before B1)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // B2: own h_t visible to every wave
+    stamp(t, 4);
+    if (sync.time_mode && chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) {
+      // end of a time chunk: publish its h rows, then wait for the next chunk's gate projection
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int c0 = chunk;
+      while (chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) ++chunk;
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int cc = c0; cc < chunk; ++cc)
+          __hip_atomic_fetch_add(sync.done + cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (chunk < sync.nr) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
+            __builtin_amdgcn_s_sleep(8);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+              if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      if (chunk < sync.nr) {  // rows t+1 and t+2 may have been prefetched before the hand-off: reload
+        __syncthreads();
+        gload(go, t + 1);
+        gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+  };
+  for (int t = 0; t < Tn; t += 2) {
+    step(t, ga, gb);
+    if (t + 1 < Tn) step(t + 1, gb, ga);
+  }  };
+  if (p == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 1>{});
+  if constexpr (ST) {
+    if (samp && Tn >= 104)
+      for (int i = 0; i < 20; ++i) g_lstm_stamps[blockIdx.x][i / 5][i % 5] = stl[i];
+  }
+  if (sync.ready && !sync.time_mode) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = ra; r <= rb; ++r) __hip_atomic_fetch_add(sync.done + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Wp[w][f = rt*8 + kg][lane][e] = W[g*256 + 64w + 16ut + (l&15)][32kg + 8(l>>4) + e],  rt = g*4 + ut
 // gate-row scale of the pre-scaled packing (lstm_cell<true>): -log2e on i / f / o, 2 log2e on g
 VAP_DEV float gate_scale(int row) { return (row >> 8) == 2 ? KC : -0.5f * KC; }
@@ -420,6 +681,22 @@ __global__ void pack_whh_resident_kernel(const float* __restrict__ whh, bf16* __
     const int rt = f >> 3, kg = f & 7, g = rt >> 2, ut = rt & 3;
     const int row = g * HD + 64 * w + 16 * ut + (l & 15);
     const int k = 32 * kg + 8 * (l >> 4) + e;
+    out[i] = (bf16)(whh[(int64_t)row * HD + k] * (pre ? gate_scale(row) : 1.0f));
+  }
+}
+
+// pair layout: Wp[p][w][f = g*8 + kk][lane][e] = W[g*256 + 128p + 16w + (l&15)][32kk + 8(l>>4) + e]
+__global__ void pack_whh_pair_kernel(const float* __restrict__ whh, bf16* __restrict__ out, int pre) {
+  const int64_t n = (int64_t)G4 * HD;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7);
+    const int l = (int)((i >> 3) & 63);
+    const int f = (int)((i >> 9) & 31);
+    const int w = (int)((i >> 14) & 7);
+    const int p = (int)(i >> 17);
+    const int g = f >> 3, kk = f & 7;
+    const int row = g * HD + 128 * p + 16 * w + (l & 15);
+    const int k = 32 * kk + 8 * (l >> 4) + e;
     out[i] = (bf16)(whh[(int64_t)row * HD + k] * (pre ? gate_scale(row) : 1.0f));
   }
 }
@@ -483,6 +760,41 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
   else if (stamps) hipLaunchKernelGGL((lstm_resident_kernel<true, false>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
   else if (prescaled) hipLaunchKernelGGL((lstm_resident_kernel<false, true>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
   else hipLaunchKernelGGL((lstm_resident_kernel<false, false>), grid, dim3(256), 0, st, gx, S, Tn, wpk, out, out_seq_stride, sy);
+  return hipGetLastError();
+}
+size_t lstm_pair_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * P_SLOT * 16; }
+int lstm_pair_workgroups(int S) { return 2 * ((S + NS - 1) / NS); }
+
+hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
+                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xepoch) {
+  if (S <= 0 || Tn <= 0 || !xbuf) return hipErrorInvalidValue;
+  LstmSync sy{};
+  if (sync) {
+    if (sync->nr < 1 || sync->nr > 16 || sync->seq_end[sync->nr - 1] < (sync->time_mode ? Tn : S))
+      return hipErrorInvalidValue;
+    for (int c = 1; c < sync->nr; ++c)
+      if (sync->seq_end[c] <= sync->seq_end[c - 1]) return hipErrorInvalidValue;
+    if (sync->gx_off < 0 || sync->gx_off >= Tn) return hipErrorInvalidValue;
+    sy = *sync;
+  }
+  sy.xepoch = xepoch;
+  static const int xplain = getenv("VAP_LSTM_XPLAIN") ? atoi(getenv("VAP_LSTM_XPLAIN")) : 0;
+  sy.xplain = xplain;
+  static const int xnowait = getenv("VAP_LSTM_XNOWAIT") ? atoi(getenv("VAP_LSTM_XNOWAIT")) : 0;  // timing diagnostics only
+  sy.xnowait = xnowait;
+  const int groups = (S + NS - 1) / NS;
+  const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
+  static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
+  if (stamps)
+    hipLaunchKernelGGL((lstm_pair_kernel<true, true>), grid, dim3(512), 0, st, gx, S, Tn, (const chunk16*)whh_pair, out,
+                       out_seq_stride, sy, (u32x4*)xbuf);
+  else
+    hipLaunchKernelGGL((lstm_pair_kernel<true, false>), grid, dim3(512), 0, st, gx, S, Tn, (const chunk16*)whh_pair, out,
+                       out_seq_stride, sy, (u32x4*)xbuf);
+  return hipGetLastError();
+}
+hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st) {
+  hipLaunchKernelGGL(pack_whh_pair_kernel, dim3(256), dim3(256), 0, st, whh, packed, 1);
   return hipGetLastError();
 }
 hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st, bool prescaled) {

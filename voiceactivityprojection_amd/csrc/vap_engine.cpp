@@ -80,6 +80,12 @@ struct vap_handle {
   // next call on the handle, vap_synchronize right away)
   unsigned* err_host = nullptr;
   unsigned* err_dev = nullptr;
+  // recurrence split over workgroup pairs (k_lstm.hip lstm_pair_kernel; VAP_LSTM_PAIR=0: one CU per
+  // 16 sequences, lstm_resident_kernel): its exchange buffer and launch epoch (exchange tags)
+  bool lstm_pair = true;
+  void* xbuf = nullptr;
+  size_t xbuf_bytes = 0;
+  unsigned xepoch = 0;
   int test_drop_ready = -1;  // VAP_TEST_DROP_READY=c (tests only): never publish ready[c] -> the wait times out
   int lstm_max_wg = 0;  // VAP_LSTM_MAX_WG: persistent recurrence launches at most this many workgroups
   unsigned epoch = 0;
@@ -132,12 +138,14 @@ struct vap_handle {
     if (streams_ready) {
       if (sync_mem) (void)hipFree(sync_mem);
       if (err_host) (void)hipHostFree(err_host);
+      if (xbuf) (void)hipFree(xbuf);
       for (auto& st : side) (void)hipStreamDestroy(st);
       for (int i = 0; i < MAXMB; ++i) {
         (void)hipEventDestroy(mb_ev[i]);
         (void)hipEventDestroy(fork_ev[i]);
       }
     }
+    if (!streams_ready && xbuf) (void)hipFree(xbuf);
     for (auto& kv : params) (void)hipFree(kv.second.dev);
     for (auto& kv : packed) (void)hipFree(kv.second);
     for (auto& kv : fpacked) (void)hipFree(kv.second);
@@ -463,6 +471,9 @@ int pack_all(vap_handle* h, hipStream_t st) {
       HIPCHK(launch_pack_wih_prescaled(h->P(p + "weight_ih" + s), (bf16*)wih, h->P(p + "bias_ih" + s),
                                        h->P(p + "bias_hh" + s), b, st));
       HIPCHK(launch_pack_whh_resident(h->P(p + "weight_hh" + s), (bf16*)whh, st, true));
+      T* whp = alloc("whh_pair" + s, 4 * D * D);  // the pair split's layout (lstm_pair_kernel)
+      if (!whp) return fail(VAP_ERR_HIP, "hipMalloc lstm");
+      HIPCHK(launch_pack_whh_pair(h->P(p + "weight_hh" + s), (bf16*)whp, st));
     } else {
       HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
       HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
@@ -761,11 +772,14 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   return VAP_OK;
 }
 
+int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* out, int64_t out_stride, hipStream_t st,
+               const LstmSync* sy, int xg0);
+
 // LSTM layer l of a clip range: input projection GEMM on `st`, recurrence on `rec_st`
 // (bf16 mode: gx bf16, W_hh resident on the CU).
 template <typename T>
 int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, hipStream_t st, hipStream_t rec_st,
-               bool recurrence = true) {
+               bool recurrence = true, int xg0 = 0) {
   const int S = r.ns();
   const int64_t L4 = p.L[4];
   const std::string s = "_l" + std::to_string(l);
@@ -788,10 +802,10 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
   }
   {
     Timed tm(h, VAP_K_LSTM_REC, rec_st);
-    if constexpr (bf)
-      HIPCHK(launch_lstm_resident((const bf16*)GX, S, (int)L4, (const bf16*)h->W<T>("whh" + s),
-                                  (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr, true));
-    else
+    if constexpr (bf) {
+      if (int rc = launch_rec(h, (const bf16*)GX, S, (int)L4, l, (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr, xg0))
+        return rc;
+    } else
       HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
   }
   return VAP_OK;
@@ -1012,7 +1026,38 @@ static int device_cus() {
 static int lstm_wg_cap(const vap_handle* h) {
   return h->lstm_max_wg > 0 ? h->lstm_max_wg : std::max(1, device_cus() / 2);
 }
-static bool persistent_fits(const vap_handle* h, int S) { return (S + 15) / 16 <= lstm_wg_cap(h); }
+// workgroups of one bf16 recurrence launch over S sequences (each publishes done counters)
+static int rec_workgroups(const vap_handle* h, int S) { return h->lstm_pair ? lstm_pair_workgroups(S) : (S + 15) / 16; }
+// groups of 16 sequences one persistent launch may take (at least one, whatever the cap)
+static int rec_group_cap(const vap_handle* h) { return std::max(1, lstm_wg_cap(h) / (h->lstm_pair ? 2 : 1)); }
+static bool persistent_fits(const vap_handle* h, int S) { return (S + 15) / 16 <= rec_group_cap(h); }
+
+// The bf16 recurrence of S sequences (gate rows GX [S][L4][1024], h rows to out): the pair split
+// (default) or the single-CU resident kernel.  xg0 offsets the launch's slots in the exchange buffer
+// (launches that may run concurrently use disjoint slots).
+int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* out, int64_t out_stride, hipStream_t st,
+               const LstmSync* sy, int xg0) {
+  const std::string s = "_l" + std::to_string(layer);
+  if (!h->lstm_pair) {
+    HIPCHK(launch_lstm_resident(GX, S, L4, h->W<bf16>("whh" + s), out, out_stride, st, sy, true));
+    return VAP_OK;
+  }
+  const size_t slot = lstm_pair_xbuf_bytes(16);
+  const size_t need = (size_t)xg0 * slot + lstm_pair_xbuf_bytes(S);
+  if (need > h->xbuf_bytes) {  // grow (rare): nothing may still use the old buffer
+    HIPCHK(hipDeviceSynchronize());
+    if (h->xbuf) HIPCHK(hipFree(h->xbuf));
+    h->xbuf = nullptr;
+    h->xbuf_bytes = 0;
+    const size_t bytes = std::max(need, (size_t)64 * slot);
+    HIPCHK(hipMalloc(&h->xbuf, bytes));
+    HIPCHK(hipMemset(h->xbuf, 0, bytes));  // tags carry the launch epoch (>= 1): zero never matches
+    h->xbuf_bytes = bytes;
+  }
+  HIPCHK(launch_lstm_pair(GX, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
+                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, ++h->xepoch));
+  return VAP_OK;
+}
 
 // VapGPT.forward pipelined ALONG TIME (bf16, 1-layer LSTM).  The frames are cut into `nch` chunks;
 // on the caller's stream the front end of chunk c computes only the conv / gate-projection rows
@@ -1135,11 +1180,11 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
   {
     Timed tm(h, VAP_K_LSTM_REC, side);
-    HIPCHK(launch_lstm_resident(GX, p.S, (int)p.L[4], h->W<bf16>("whh_l0"), (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, true));
+    if (int rc = launch_rec(h, GX, p.S, (int)p.L[4], 0, (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
   }
   // the back ends wait for these counts: raise them only once the launch is in the queue (a failed
   // launch must not leave later forwards waiting for arrivals that never come)
-  const int nwg = (p.S + 15) / 16;  // launch_lstm_resident: 16 sequences per workgroup
+  const int nwg = rec_workgroups(h, p.S);
   for (int c = 0; c < t.nch; ++c) h->done_expect[c] += nwg;
   return VAP_OK;
 }
@@ -1339,7 +1384,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       int rc;
       if ((rc = h->ensure_streams())) return rc;
       if (h->wait_value) {
-        const int per = std::max(1, lstm_wg_cap(h) * 16 / 2);  // clips per slice (2 sequences each)
+        const int per = std::max(1, rec_group_cap(h) * 16 / 2);  // clips per slice (2 sequences each)
         const int ns = (B + per - 1) / per;
         for (int i = 0; i < ns; ++i) {
           const int c0 = (int)((int64_t)B * i / ns), c1 = (int)((int64_t)B * (i + 1) / ns);
@@ -1404,13 +1449,14 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       sy.nr = nr;
       for (int i = 0; i < nr; ++i) sy.seq_end[i] = 2 * (rs[i].c0 + rs[i].nc);
       unsigned add[vap_handle::MAXMB] = {};
-      for (int wg = 0; wg * 16 < S; ++wg) {  // done increments per range (launch_lstm_resident: 16 sequences per WG)
+      const unsigned per_grp = h->lstm_pair ? 2u : 1u;  // workgroups per 16 sequences
+      for (int wg = 0; wg * 16 < S; ++wg) {  // done increments per range (16 sequences per group)
         const int s_first = wg * 16, s_last = std::min(S, s_first + 16) - 1;
         int ra = 0;
         while (sy.seq_end[ra] <= s_first) ++ra;
         int rb = ra;
         while (sy.seq_end[rb] <= s_last) ++rb;
-        for (int r = ra; r <= rb; ++r) ++add[r];
+        for (int r = ra; r <= rb; ++r) add[r] += per_grp;
       }
       hipStream_t side = h->side[0];
       hipEvent_t fork = h->next_fork_event();
@@ -1418,8 +1464,9 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       HIPCHK(hipStreamWaitEvent(side, fork, 0));
       {
         Timed tm(h, VAP_K_LSTM_REC, side);
-        HIPCHK(launch_lstm_resident((const bf16*)(ws + p.GX), S, (int)L[4], (const bf16*)h->W<T>("whh_l0"),
-                                    (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh, side, &sy, true));
+        if ((rc = launch_rec(h, (const bf16*)(ws + p.GX), S, (int)L[4], 0, (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh,
+                             side, &sy, 0)))
+          return rc;
       }
       for (int i = 0; i < nr; ++i) h->done_expect[i] += add[i];  // only after a successful launch
       for (int i = 0; i < nr; ++i) {
@@ -1436,10 +1483,12 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       return VAP_OK;
     }
   }
+  int xg0 = 0;  // concurrent per-range recurrences use disjoint exchange slots
   for (size_t i = 0; i < rs.size(); ++i) {
     if ((rc = front_end<T>(h, p, wav, N, ws, rs[i], st))) return rc;
     hipStream_t side = h->side[i % vap_handle::NSIDE];
-    if ((rc = lstm_layer<T>(h, p, ws, 0, rs[i], st, side))) return rc;
+    if ((rc = lstm_layer<T>(h, p, ws, 0, rs[i], st, side, true, xg0))) return rc;
+    xg0 += (rs[i].ns() + 15) / 16;
     HIPCHK(hipEventRecord(h->mb_ev[i], side));
   }
   for (size_t i = 0; i < rs.size(); ++i) {
@@ -1575,12 +1624,12 @@ int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, floa
   sy.time_mode = 1;
   for (int c = 0; c < t.nch; ++c) sy.seq_end[c] = t.seq_end[c];
   unsigned expect[vap_handle::MAXMB];
-  for (int c = 0; c < t.nch; ++c) expect[c] = (unsigned)((S + 15) / 16);  // launch_lstm_resident: 16 sequences / WG
+  for (int c = 0; c < t.nch; ++c) expect[c] = (unsigned)rec_workgroups(h, S);
   hipStream_t side = h->side[0];
   hipEvent_t fork = h->next_fork_event();
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
-  HIPCHK(launch_lstm_resident(s->gx, S, (int)L4, h->W<bf16>("whh_l0"), (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy, true));
+  if (int rc = launch_rec(h, s->gx, S, (int)L4, 0, (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
   // captured: everything else on the caller's stream
   const vap_stream::GKey key{off, nxt, logits, vadl};
   auto it = s->graphs.find(key);
@@ -1734,6 +1783,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
+  if (const char* e = getenv("VAP_LSTM_PAIR")) h->lstm_pair = atoi(e) != 0;
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;

@@ -75,12 +75,23 @@ struct LstmSync {
                      // done[c] after it)
   int time_mode;
   int gx_off = 0;    // gate rows form a ring: step t reads gx row (t + gx_off) mod Tn (streaming)
+  unsigned xepoch = 0;  // lstm_pair: launch epoch in the exchange tags (set by launch_lstm_pair)
+  int xplain = 0;       // lstm_pair: exchange stores with the default policy (experiment)
+  int xnowait = 0;      // lstm_pair: do not wait for the partner (timing diagnostics; outputs are garbage)
 };
 // prescaled: W_ih / W_hh / biases packed with the gate scales (launch_pack_wih_prescaled,
 // launch_pack_whh_resident(.., true)): gates arrive as -log2e (i, f, o) / 2 log2e (g) multiples
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
                                 int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, bool prescaled = false);
 hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t st, bool prescaled = false);
+// W_hh split over a pair of workgroups (k_lstm.hip lstm_pair_kernel): pre-scaled packing, the
+// exchange buffer it needs for S sequences (zeroed once; tags carry the launch epoch, which must
+// differ between launches that share the buffer), and the workgroups one launch runs
+hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
+                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xepoch);
+hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
+size_t lstm_pair_xbuf_bytes(int S);
+int lstm_pair_workgroups(int S);
 hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st);
 hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,
                                      hipStream_t st);

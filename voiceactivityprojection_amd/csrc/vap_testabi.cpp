@@ -88,6 +88,26 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
     (void)hipFree(gs);
     return rc_of(e);
   }
+  if (precision == VAP_PRECISION_BF16 && variant == 3) {  // the pair split (lstm_pair_kernel), pre-scaled
+    void* gs = nullptr;
+    void* xb = nullptr;
+    const int64_t n = (int64_t)S * T * 1024;
+    const size_t xbytes = lstm_pair_xbuf_bytes(S);
+    if (hipMalloc(&gs, n * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+    if (hipMalloc(&xb, xbytes) != hipSuccess) {
+      (void)hipFree(gs);
+      return VAP_ERR_HIP;
+    }
+    hipError_t e = hipMemsetAsync(xb, 0, xbytes, st);
+    if (e == hipSuccess) e = launch_pack_whh_pair(whh, (bf16*)whh_packed, st);
+    if (e == hipSuccess) e = launch_scale_gates((const bf16*)gx, (bf16*)gs, n, st);
+    if (e == hipSuccess)
+      e = launch_lstm_pair((const bf16*)gs, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr, xb, 1);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(gs);
+    (void)hipFree(xb);
+    return rc_of(e);
+  }
   if (precision == VAP_PRECISION_BF16 && variant == 0) {
     hipError_t e = launch_pack_whh_resident(whh, (bf16*)whh_packed, st);
     if (e != hipSuccess) return VAP_ERR_HIP;
