@@ -175,6 +175,8 @@ def main():
     ap.add_argument("--which", default="rowpanel,attn")
     ap.add_argument("--case", default="", help="only GEMM cases whose name contains this")
     ap.add_argument("--packed", action="store_true", help="row-panel W in the packed layout")
+    ap.add_argument("--attn-seqs", type=int, default=32, help="sequences of the attention benchmark")
+    ap.add_argument("--attn-frames", type=int, default=1000)
     args = ap.parse_args()
     lib = _native.lib()
     dev = torch.device("cuda:0")
@@ -187,7 +189,7 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
     if "attn" in args.which:
-        res.update(bench_attn(lib, dev, st, args.iters))
+        res.update(bench_attn(lib, dev, st, args.iters, S=args.attn_seqs, T=args.attn_frames))
     if "ffn" in args.which:
         res.update(bench_ffn(lib, dev, st, args.iters, args.rows))
     if "gemm" in args.which:

@@ -1,5 +1,7 @@
 // Memory-bound kernels of the VAP path: conv0 + ChannelNorm + ReLU, LayerNorm, the
 // va_classifier head, the probs() epilogue and label extraction + cross entropy.
+#include <algorithm>
+
 #include "vap_common.h"
 #include "vap_kernels.h"
 
@@ -88,6 +90,15 @@ __global__ void zero_rows_kernel(T* base, int64_t seq_stride, int rows) {
   T* p = base + (int64_t)s * seq_stride;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = from_f32<T>(0.f);
+}
+
+// every region's pad rows in one launch: region r = blockIdx.z, sequence = blockIdx.y
+__global__ void zero_regions_kernel(ZeroRegions z) {
+  const ZeroRegion& r = z.r[blockIdx.z];
+  const int64_t n = r.bytes / 16;  // 16-byte words per sequence (rows x 256 x element size)
+  unsigned char* p = (unsigned char*)r.base + (int64_t)blockIdx.y * r.seq_stride_bytes;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ((u32x4*)p)[i] = u32x4{0u, 0u, 0u, 0u};
 }
 
 // ------------------------------------------------------------------------------------------
@@ -337,6 +348,18 @@ hipError_t launch_zero_rows(T* base, int n_seq, int64_t seq_stride, int rows, hi
   const int64_t n = (int64_t)rows * 256;
   dim3 grid((unsigned)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64), n_seq);
   hipLaunchKernelGGL((zero_rows_kernel<T>), grid, dim3(256), 0, st, base, seq_stride, rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_zero_regions(const ZeroRegions& z, int n_seq, hipStream_t st) {
+  if (z.n <= 0 || z.n > ZeroRegions::MAX || n_seq <= 0) return hipErrorInvalidValue;
+  int64_t most = 0;
+  for (int i = 0; i < z.n; ++i) {
+    if (z.r[i].bytes % 16 || z.r[i].seq_stride_bytes % 16 || ((uintptr_t)z.r[i].base & 15)) return hipErrorInvalidValue;
+    most = std::max<int64_t>(most, z.r[i].bytes / 16);
+  }
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(8, (most + 255) / 256)), n_seq, z.n);
+  hipLaunchKernelGGL(zero_regions_kernel, grid, dim3(256), 0, st, z);
   return hipGetLastError();
 }
 

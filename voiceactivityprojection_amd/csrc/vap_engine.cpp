@@ -57,7 +57,9 @@ struct vap_handle {
   double tc_edge = 0.0;             // time chunks: first / last chunk fraction of the frames (0: even split)
   // forward: front-end / back-end boundaries (cumulative frame fractions, VAP_TC_FE / VAP_TC_BE;
   // "" = the even time_chunks split for both)
-  std::vector<double> tc_fe{0.1, 0.24, 0.4, 0.7}, tc_be{0.384, 0.768, 0.896};
+  // (the pair-split recurrence ends well before the caller stream's work: two back-end chunks, the
+  // first of 640 frames = 5 full 128-query attention blocks, measured best: 156.2k -> 166.3k audio-s/s)
+  std::vector<double> tc_fe{0.1, 0.25, 0.45, 0.7}, tc_be{0.64};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
   bool heads_chunked = false;  // VAP_HEADS_CHUNKED=1: heads per back-end chunk (shorter tail after the
                                // recurrence, but small GEMMs: 0.41 vs 0.19 ms; the caller stream binds)
@@ -1396,20 +1398,25 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       }
     }
   }
-  // pad rows (conv zero padding lives in explicit rows)
-  if constexpr (sizeof(T) == 4) {  // bf16 mode never materialises conv0
-    T* X0 = (T*)(ws + p.X0);
-    HIPCHK(launch_zero_rows<T>(X0, S, p.s0, 2, st));
-    HIPCHK(launch_zero_rows<T>(X0 + (L[0] + 2) * D, S, p.s0, 2, st));
+  // pad rows (conv zero padding lives in explicit rows), every region in one launch
+  {
+    constexpr int64_t R = D * (int64_t)sizeof(T);  // bytes per row
+    ZeroRegions z;
+    if constexpr (sizeof(T) == 4) {  // bf16 mode never materialises conv0
+      T* X0 = (T*)(ws + p.X0);
+      z.add(X0, p.s0 * sizeof(T), 2 * R);
+      z.add(X0 + (L[0] + 2) * D, p.s0 * sizeof(T), 2 * R);
+    }
+    T* Xz[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
+    const int64_t sz[4] = {p.s1, p.s2, p.s3, p.s4};
+    for (int i = 0; i < 4; ++i) {
+      z.add(Xz[i], sz[i] * sizeof(T), R);
+      z.add(Xz[i] + (L[i + 1] + 1) * D, sz[i] * sizeof(T), R);
+    }
+    z.add(ws + p.H0, p.sh * sizeof(T), 4 * R);
+    z.add(ws + p.H1, p.sh * sizeof(T), 4 * R);
+    HIPCHK(launch_zero_regions(z, S, st));
   }
-  T* Xs[4] = {(T*)(ws + p.X1), (T*)(ws + p.X2), (T*)(ws + p.X3), (T*)(ws + p.X4)};
-  const int64_t ss[4] = {p.s1, p.s2, p.s3, p.s4};
-  for (int i = 0; i < 4; ++i) {
-    HIPCHK(launch_zero_rows<T>(Xs[i], S, ss[i], 1, st));
-    HIPCHK(launch_zero_rows<T>(Xs[i] + (L[i + 1] + 1) * D, S, ss[i], 1, st));
-  }
-  HIPCHK(launch_zero_rows<T>((T*)(ws + p.H0), S, p.sh, 4, st));
-  HIPCHK(launch_zero_rows<T>((T*)(ws + p.H1), S, p.sh, 4, st));
 
   const int NL = h->dims.lstm_layers;
   int m = h->microbatches < 1 ? 1 : h->microbatches;

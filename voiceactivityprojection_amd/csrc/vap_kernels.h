@@ -46,6 +46,19 @@ hipError_t launch_va_cond(float* x, const float* va, const float* hist, int rows
 // Zero `rows` rows of width 256 at `base + s*seq_stride` for every sequence (pad rows).
 template <typename T>
 hipError_t launch_zero_rows(T* base, int n_seq, int64_t seq_stride, int rows, hipStream_t st);
+// several per-sequence byte ranges zeroed in ONE launch (the conv / LSTM pad rows of a forward)
+struct ZeroRegion {
+  void* base;
+  int64_t seq_stride_bytes;
+  int64_t bytes;  // per sequence, multiple of 16
+};
+struct ZeroRegions {
+  static constexpr int MAX = 16;
+  ZeroRegion r[MAX];
+  int n = 0;
+  void add(void* base, int64_t seq_stride_bytes, int64_t bytes) { r[n++] = ZeroRegion{base, seq_stride_bytes, bytes}; }
+};
+hipError_t launch_zero_regions(const ZeroRegions& z, int n_seq, hipStream_t st);
 
 // LayerNorm over 256 (biased var) of fp32 rows -> T, optional raw fp32->T copy.
 template <typename T>
