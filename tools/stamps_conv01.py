@@ -32,7 +32,7 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros((8, 24), dtype=np.uint64)
     N.check(N.lib().vap_test_read_stamps(ctypes.c_void_p(buf.ctypes.data)))
-    if not any(os.environ.get(f"VAP_CONV01_V{v}") for v in (2, 4)):
+    if not any(os.environ.get(f"VAP_CONV01_V{v}") for v in (2, 4)):  # v9 / v10 (default)
         # v5: start | prologue | units 0-7, 8-15, 16-23, 24-31 | epilogue
         names, n = ["prologue", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 7
     elif os.environ.get("VAP_CONV01_V4"):  # v4: start | prologue | units 0-7, 8-15, 16-23, 24-31 | epilogue

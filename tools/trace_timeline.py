@@ -9,7 +9,7 @@ import sys
 
 
 def short(n):
-    for k in ("lstm_resident", "conv01", "gemm2_kernelIDF16b", "gemm2_kernel<float", "attn3", "block_kernel",
+    for k in ("lstm_pair", "lstm_resident", "conv01", "gemm2_kernelIDF16b", "gemm2_kernel<float", "attn3", "block_kernel",
               "lnproj_kernel", "rowpanel", "streamOpsWait", "streamOpsWrite", "probs", "labels", "vad_head",
               "zero_rows", "copyBuffer", "layernorm"):
         if k in n:
@@ -21,14 +21,14 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"]) for r in rows]
     ks.sort()
-    lstm = [k for k in ks if k[2] == "lstm_resident"]
+    lstm = [k for k in ks if k[2] in ("lstm_resident", "lstm_pair")]
     L = lstm[-2] if len(lstm) > 1 else lstm[-1]  # the last timed forward (the very last may be a breakdown pass)
     t0 = L[0]
     win = [k for k in ks if k[0] >= L[0] - 3_000_000 and k[0] <= L[1] + 3_000_000]
     prev_end = None
     print(f"LSTM {L[0]-t0} .. {(L[1]-t0)/1e3:.1f} us (queue {L[3]})")
     for s, e, n, q in win:
-        if n == "lstm_resident":
+        if n in ("lstm_resident", "lstm_pair"):
             continue
         gap = "" if prev_end is None else f" gap {(s - prev_end)/1e3:7.1f}"
         print(f"{(s - t0)/1e3:9.1f} {(e - t0)/1e3:9.1f} {(e - s)/1e3:8.1f} q{q} {n}{gap}")

@@ -715,6 +715,326 @@ __global__ __launch_bounds__(256, 1) void conv01i_kernel(const float* __restrict
 }
 
 
+// ------------------------------------------------------------------------------------------
+// v10 (default): v9's slice pipeline with EIGHT waves, two per SIMD.
+// v9 runs one wave per SIMD, so everything that is not an MFMA -- the slice production (SV reads,
+// conv0 MFMAs, ReLU / packing, LDS stores), the W1 loads, the unit barriers -- sits in the one
+// instruction stream of its SIMD: 3.4k cycles per unit against 2,048 of MFMA.  Here wave w owns
+// output channels 32w .. 32w+31 for all 256 rows (16 x 2 MFMA tiles, 128 accumulators in AGPRs, so
+// two waves fit a SIMD's 512 registers) and the partner wave's MFMAs fill the gaps one wave leaves.
+//   * W1 fragments stay unique per wave (no wave pair shares a column), so the L2 W1 stream is v9's;
+//     each G fragment now feeds two MFMAs instead of four (LDS reads 128 B / cycle / CU at the MFMA
+//     rate, half the array's peak);
+//   * slice work is split by (channel tile ct = w & 1, position tiles w/2 + 4x; waves 0 and 1 also
+//     make tile 16): 4-5 conv0 MFMAs per wave and unit instead of 10;
+//   * ChannelNorm-1 row statistics reduce over 8 partials (one per wave) through LDS.
+// Same per-accumulator k order as v9 (only the ChannelNorm partial sums are grouped differently).
+// ------------------------------------------------------------------------------------------
+constexpr int K_OFF_G = 0;                                    // 3 slots of 272 x 64 B
+constexpr int K_OFF_RED = 3 * I_GSLOT;                        // 52224: [256 rows][8 waves] f32 (epilogue)
+constexpr int K_OFF_WV = 2 * I_GSLOT;                         // 34816: over slot 2 + red (prologue)
+constexpr int K_OFF_SV = K_OFF_RED + BM2 * 8 * 4;             // 60416
+constexpr int K_OFF_C0 = K_OFF_SV + I_SVN * 64;               // 130048
+constexpr int K_OFF_BE = K_OFF_C0 + 256 * 64;                 // 146432
+constexpr int K_LDS = K_OFF_BE + 4 * 256 * 4;                 // 150528
+static_assert(K_OFF_WV + WSEG2 * 4 <= K_OFF_SV, "conv01 v10 waveform alias");
+static_assert(K_LDS <= 163840, "conv01 v10 LDS");
+
+template <bool STAMPS>
+__global__ __launch_bounds__(512, 1) void conv01k_kernel(const float* __restrict__ wav, int64_t N, int L0,
+                                                        const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
+                                                        const float* __restrict__ beta0, const bf16* __restrict__ W1,
+                                                        const float* __restrict__ b1, const float* __restrict__ g1,
+                                                        const float* __restrict__ be1, bf16* __restrict__ out,
+                                                        int64_t out_seq_stride, int r0, int r1) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[K_LDS];
+  unsigned char* G = smem + K_OFF_G;
+  unsigned char* SV = smem + K_OFF_SV;
+  unsigned char* C0 = smem + K_OFF_C0;
+  float* BE = (float*)(smem + K_OFF_BE);
+  float* EP = BE + 256;
+  float* WV = (float*)(smem + K_OFF_WV);
+  float* red = (float*)(smem + K_OFF_RED);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32w..32w+31, all 256 rows
+  const int ct = w & 1, pq = w >> 1;                        // slice work: channel tile, position tiles pq + 4x
+  const bool p16 = w < 2;                                   // ... and tile 16 (rows 256.., read by row 255 only)
+  const int s = blockIdx.y;
+  const int t0 = r0 + blockIdx.x * BM2;
+  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
+  unsigned long long stv[8];
+  int nst = 0;
+  auto stamp = [&]() {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (nst < 8) stv[nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp();
+
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W1, 64 * 256 * 64);
+  const uint32_t wlo = (uint32_t)(((w * 32 + (lane & 15)) * 4 + (lane >> 4)) * 16);
+  auto wload = [&](int u, chunk16* wf) {  // unit u: [h * 2 + j] = k-step (u, h), column tile j
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = ((u >> 3) + 4 * h) * 8 + (u & 7);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[h * 2 + j] = buf_load16(wrs, wlo, (uint32_t)(kk * 16384 + j * 1024));
+    }
+  };
+
+  // ---------------- prologue
+  {
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(wav + (int64_t)s * N, (uint32_t)(N * 4));
+    const int xb = 20 * t0 - 13;  // first sample of the segment (negative offsets read as zero)
+    uint32_t wv[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+      wv[k] = __builtin_amdgcn_raw_buffer_load_b32(wr, (int)((uint32_t)(xb + tid + 512 * k) * 4u), 0, 0);
+    chunk16 c0[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) c0[i] = c0w[tid + i * 512];
+    f32x4 ep = {0.f, 0.f, 0.f, 0.f};
+    if (tid < 64) ep = ((const f32x4*)beta0)[tid];
+    else if (tid < 128) ep = ((const f32x4*)b1)[tid - 64];
+    else if (tid < 192) ep = ((const f32x4*)g1)[tid - 128];
+    else if (tid < 256) ep = ((const f32x4*)be1)[tid - 192];
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+      if (tid + 512 * k < WSEG2) WV[tid + 512 * k] = __builtin_bit_cast(float, wv[k]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ((chunk16*)C0)[tid + i * 512] = c0[i];
+    if (tid < 256) ((f32x4*)BE)[tid] = ep;
+  }
+  chunk16 W[3][4];  // W1 register ring: unit u in set u % 3
+  wload(0, W[0]);
+  wload(1, W[1]);
+  __syncthreads();
+
+  for (int j = tid; j < I_SVN; j += 512) {
+    const int r = j / NPOS2, i = j - r * NPOS2;
+    const int p = 4 * (t0 + i) - 2 + r;
+    const bool valid = i < GROWS2 && p >= 0 && p < L0;
+    float sm[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG2 - 1)];
+    float q = c0stat[C0Stat::BETA];
+#pragma unroll
+    for (int a = 0; a < 10; ++a) {
+      float ga = fmaf(c0stat[C0Stat::G + a * 10 + a], sm[a], 2.0f * c0stat[C0Stat::H + a]);
+#pragma unroll
+      for (int b = a + 1; b < 10; ++b) ga = fmaf(2.0f * c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
+      q = fmaf(ga, sm[a], q);
+    }
+    const float rs = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : 0.f;
+    bf16 hi[10], lo[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const float x = rs * sm[k];
+      hi[k] = (bf16)x;
+      lo[k] = (bf16)(x - (float)hi[k]);
+    }
+    const bf16 rb = (bf16)rs;
+    const bf16x8 v[4] = {{hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]},
+                         {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]},
+                         {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]},
+                         {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], rb, rb}};
+    unsigned char* row = SV + j * 64;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(bf16x8*)(row + sphys(j, c) * 16) = v[c];
+  }
+
+  // validity of this lane's position in slice tile x (pq + 4x, x < 4; 16 for x = 4) of phase r: bit 5r + x
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      const int pt = x == 4 ? 16 : pq + 4 * x;
+      const int p = 4 * (t0 + pt * 16 + (lane & 15)) - 2 + r;
+      vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
+    }
+  __syncthreads();
+
+  // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; this wave makes channel tile ct
+  auto read_c0 = [&](int v, chunk16& c0, f32x4& bt) {
+    const int g = v & 7;
+    c0 = ((const chunk16*)C0)[((2 * g + ct) * 16 + (lane & 15)) * 4 + (lane >> 4)];
+    bt = *(const f32x4*)(BE + (2 * g + ct) * 16 + 4 * (lane >> 4));
+  };
+  auto read_sv = [&](int v, int x) -> chunk16 {
+    const int pt = x == 4 ? 16 : pq + 4 * x;
+    const int jj = ((v >> 3) & 3) * NPOS2 + pt * 16 + (lane & 15);
+    return *(const chunk16*)(SV + jj * 64 + sphys(jj, lane >> 4) * 16);
+  };
+  auto pstore = [&](int v, int x, const f32x4& z) {
+    const int pt = x == 4 ? 16 : pq + 4 * x;
+    const int prow = pt * 16 + (lane & 15);
+    const uint32_t m = 0u - ((vmask >> (5 * ((v >> 3) & 3) + x)) & 1u);
+    unsigned char* gs = G + (v % 3) * I_GSLOT;
+    const u32x2 o = {relu_bf16x2(z[0], z[1]) & m, relu_bf16x2(z[2], z[3]) & m};
+    const int lc = 2 * ct + (lane >> 5);
+    *(u32x2*)(gs + prow * 64 + sphys(prow, lc) * 16 + ((lane >> 4) & 1) * 8) = o;
+  };
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {  // slices 0 and 1
+    chunk16 c0;
+    f32x4 bt;
+    read_c0(v, c0, bt);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      if (x == 4 && !p16) break;
+      const chunk16 sv = read_sv(v, x);
+      pstore(v, x, mfma_chunk<bf16>(c0, sv, bt));
+    }
+  }
+
+  f32x4 acc[2][16];  // [n tile][m tile] of C^T, in AGPRs
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto gread = [&](int u, int n) -> chunk16 {  // n = 16h + i -> k-step (u,h), row block i
+    const unsigned char* gs = G + (u % 3) * I_GSLOT;
+    const int row = (n & 15) * 16 + (lane & 15) + (n >> 4);
+    return *(const chunk16*)(gs + row * 64 + sphys(row, lane >> 4) * 16);
+  };
+  chunk16 gf[4];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // slices 0, 1 published; WV (slot 2) free
+#pragma unroll
+  for (int n = 0; n < 3; ++n) gf[n] = gread(0, n);
+  stamp();
+
+  auto unit = [&](const int u, chunk16* wf, chunk16* wn2, const bool last1, const bool last2) {
+    // B_u: own slice u+1 stores retired; W1 of unit u landed (unit u+1's 4 loads are younger)
+    __builtin_amdgcn_sched_barrier(0);
+    if (last1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (!last2) wload(u + 2, wn2);
+    const int v = u + 2;
+    chunk16 c0, sv;
+    f32x4 bt, z;
+    read_c0(v, c0, bt);
+#pragma unroll
+    for (int n = 0; n < 32; ++n) {
+      __builtin_amdgcn_sched_barrier(0);
+      // slice v: tile x operands at group 7x, MFMA at 7x+2, store at 7x+4 (tile 16: 28 / 30 / 31)
+      if (n % 7 == 0 && n / 7 < 4) sv = read_sv(v, n / 7);
+      if (n % 7 == 2 && n / 7 < 4) z = mfma_chunk<bf16>(c0, sv, bt);
+      if (n % 7 == 4 && n / 7 < 4) pstore(v, n / 7, z);
+      if (p16) {
+        if (n == 28) sv = read_sv(v, 4);
+        if (n == 30) z = mfma_chunk<bf16>(c0, sv, bt);
+        if (n == 31) pstore(v, 4, z);
+      }
+      const int i = n & 15, h = n >> 4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) mfma_acc(acc[j][i], wf[2 * h + j], gf[n & 3]);
+      if (n + 3 < 32) gf[(n + 3) & 3] = gread(u, n + 3);
+      else if (!last1) gf[(n + 3) & 3] = gread(u + 1, n + 3 - 32);
+    }
+    if ((u & 7) == 7) stamp();
+  };
+  for (int u = 0; u < 30; u += 3) {
+    unit(u, W[0], W[2], false, false);
+    unit(u + 1, W[1], W[0], false, false);
+    unit(u + 2, W[2], W[1], false, u + 2 >= 30);
+  }
+  unit(30, W[0], W[2], false, true);
+  unit(31, W[1], W[0], true, true);
+
+  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[m = i*16 + lane%16][n = 32w + j*16 + (lane/16)*4 + e]
+#pragma unroll
+  for (int j = 0; j < 2; ++j)  // MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(acc[j][0]), "+a"(acc[j][1]), "+a"(acc[j][2]), "+a"(acc[j][3]), "+a"(acc[j][4]),
+                   "+a"(acc[j][5]), "+a"(acc[j][6]), "+a"(acc[j][7]), "+a"(acc[j][8]), "+a"(acc[j][9]),
+                   "+a"(acc[j][10]), "+a"(acc[j][11]), "+a"(acc[j][12]), "+a"(acc[j][13]), "+a"(acc[j][14]),
+                   "+a"(acc[j][15]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live)
+  const int nb = w * 32 + (lane >> 4) * 4;
+  f32x4 bb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bb[j] = *(const f32x4*)(EP + nb + j * 16);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 t = acc[0][i] + bb[0] + acc[1][i] + bb[1];
+    float sum = t[0] + t[1] + t[2] + t[3];
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 8 + w] = sum;
+  }
+  __syncthreads();
+  float mean[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 pa = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8);
+    const f32x4 pb = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8 + 4);
+    mean[i] = ((pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]))) * (1.0f / BN);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 d0 = acc[0][i] + bb[0] - mean[i], d1 = acc[1][i] + bb[1] - mean[i];
+    const f32x4 t = d0 * d0 + d1 * d1;
+    float ss = t[0] + t[1] + t[2] + t[3];
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 8 + w] = ss;
+  }
+  __syncthreads();
+  f32x4 gg[2], ee[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    gg[j] = *(const f32x4*)(EP + 256 + nb + j * 16);
+    ee[j] = *(const f32x4*)(EP + 512 + nb + j * 16);
+  }
+  // 16-B stores: v_permlane16_swap trades column block 1 of even row groups for block 0 of odd ones,
+  // so even groups own 8 consecutive channels of block 0, odd groups of block 1
+  bf16* obase = out + (int64_t)s * out_seq_stride;
+  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
+  const int R = lane >> 4;
+  const int col = w * 32 + (R & 1) * 16 + (R >> 1) * 8;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f32x4 pa = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8);
+    const f32x4 pb = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8 + 4);
+    const float var = (pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
+    const float rstd = rsqrtf(var * (1.0f / (BN - 1)) + 1e-5f);
+    const int t = t0 + i * 16 + (lane & 15);
+    uint32_t pk[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const f32x4 v = (acc[j][i] + bb[j] - mean[i]) * rstd * gg[j] + ee[j];
+      pk[j][0] = relu_bf16x2(v[0], v[1]);
+      pk[j][1] = relu_bf16x2(v[2], v[3]);
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][d], pk[1][d], false, false);
+      pk[0][d] = sw[0];
+      pk[1][d] = sw[1];
+    }
+    const u32x4 o = {pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
+    buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
+  }
+  if constexpr (STAMPS) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+    if (samp >= 0 && tid == 0)
+      for (int k = 0; k < 8 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
@@ -738,6 +1058,16 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
     return hipGetLastError();
   }
   dim3 grid((r1 - r0 + BM2 - 1) / BM2, S);
+  static const bool v9 = getenv("VAP_CONV01_V9") != nullptr;  // the four-wave kernel (previous default)
+  if (!v9) {
+    if (stamps)
+      hipLaunchKernelGGL(conv01k_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
+                         b1, g1, be1, out, out_seq_stride, r0, r1);
+    else
+      hipLaunchKernelGGL(conv01k_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s, b1,
+                       g1, be1, out, out_seq_stride, r0, r1);
+    return hipGetLastError();
+  }
   static const int diag = getenv("VAP_CONV01_DIAG") ? atoi(getenv("VAP_CONV01_DIAG")) : 0;
   if (stamps && diag) {  // timing diagnostics only: the outputs are garbage
 #define VAP_DIAG_CASE(D)                                                                                          \
