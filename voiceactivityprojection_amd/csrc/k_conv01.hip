@@ -22,6 +22,7 @@
 // G = Wc^T Wc (10x10), h = Wc^T bc, beta = bc.bc  (Wc, bc = centred conv0 weights / bias), so the
 // statistics need no pass over the 256 channels.  Padding positions (p < 0 or p >= L0) are zero rows.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "vap_common.h"
@@ -1035,6 +1036,332 @@ __global__ __launch_bounds__(512, 1) void conv01k_kernel(const float* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// v11 (default): v10 with the conv1 k-steps on v_mfma_f32_32x32x16_bf16.
+// v10's units ran at ~71 % of MFMA issue, issue-bound: a 16x16x32 MFMA leaves 8 of its 16 cycles to
+// the SIMD's other instructions, and a unit carries ~100 of them per wave (G reads, waits, slice
+// work).  A 32x32x16 leaves 24 of 32 for the same k-work (half the MFMA instructions, the same G /
+// W1 fragment count: a 32-row x 16-k fragment is 1 KiB like a 16 x 32 one).
+//   * wave w: 8 row tiles of 32 x one 32-channel column tile (8 x 16 accumulators in AGPRs);
+//   * G slots use the swizzle chunk' = (chunk + row/4) mod 4: conflict-free ds_read_b128 for 32
+//     consecutive rows (either tap offset) and for the slice stores of 16 rows (v10's swizzle was
+//     2-way conflicted on the stores);
+//   * epilogue rows are one lane each (row = lane % 32 of a row tile, 16 channels per lane, the
+//     other 16 in lane ^ 32): row sums by one shuffle, 16-B stores via v_permlane32_swap.
+// ------------------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+VAP_DEV int gphys(int row, int c) { return (c + (row >> 2)) & 3; }
+VAP_DEV void mfma32_acc(f32x16& c, const chunk16& a, const chunk16& b) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+
+template <bool STAMPS>
+__global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict__ wav, int64_t N, int L0,
+                                                        const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
+                                                        const float* __restrict__ beta0, const bf16* __restrict__ W1,
+                                                        const float* __restrict__ b1, const float* __restrict__ g1,
+                                                        const float* __restrict__ be1, bf16* __restrict__ out,
+                                                        int64_t out_seq_stride, int r0, int r1) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[K_LDS];
+  unsigned char* G = smem + K_OFF_G;
+  unsigned char* SV = smem + K_OFF_SV;
+  unsigned char* C0 = smem + K_OFF_C0;
+  float* BE = (float*)(smem + K_OFF_BE);
+  float* EP = BE + 256;
+  float* WV = (float*)(smem + K_OFF_WV);
+  float* red = (float*)(smem + K_OFF_RED);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32w..32w+31, all 256 rows
+  const int ct = w & 1, pq = w >> 1;                        // slice work: channel tile, position tiles pq + 4x
+  const bool p16 = w < 2;                                   // ... and tile 16 (rows 256.., read by row 255 only)
+  const int s = blockIdx.y;
+  const int t0 = r0 + blockIdx.x * BM2;
+  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
+  unsigned long long stv[8];
+  int nst = 0;
+  auto stamp = [&]() {
+    if constexpr (STAMPS) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (nst < 8) stv[nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp();
+
+  // W1 fragment (A of the 32x32x16): channel 32w + lane%32, k 16kh + 8(lane/32) of a 32-deep k-step
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W1, 64 * 256 * 64);
+  const uint32_t wlo = (uint32_t)((w * 32 + (lane & 31)) * 64 + (lane >> 5) * 16);
+  auto wload = [&](int u, chunk16* wf) {  // unit u: [h * 2 + kh] = k-step (u, h), k half kh
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = ((u >> 3) + 4 * h) * 8 + (u & 7);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) wf[h * 2 + kh] = buf_load16(wrs, wlo, (uint32_t)(kk * 16384 + kh * 32));
+    }
+  };
+
+  // ---------------- prologue
+  {
+    const __amdgpu_buffer_rsrc_t wr = make_rsrc(wav + (int64_t)s * N, (uint32_t)(N * 4));
+    const int xb = 20 * t0 - 13;  // first sample of the segment (negative offsets read as zero)
+    uint32_t wv[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+      wv[k] = __builtin_amdgcn_raw_buffer_load_b32(wr, (int)((uint32_t)(xb + tid + 512 * k) * 4u), 0, 0);
+    chunk16 c0[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) c0[i] = c0w[tid + i * 512];
+    f32x4 ep = {0.f, 0.f, 0.f, 0.f};
+    if (tid < 64) ep = ((const f32x4*)beta0)[tid];
+    else if (tid < 128) ep = ((const f32x4*)b1)[tid - 64];
+    else if (tid < 192) ep = ((const f32x4*)g1)[tid - 128];
+    else if (tid < 256) ep = ((const f32x4*)be1)[tid - 192];
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+      if (tid + 512 * k < WSEG2) WV[tid + 512 * k] = __builtin_bit_cast(float, wv[k]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ((chunk16*)C0)[tid + i * 512] = c0[i];
+    if (tid < 256) ((f32x4*)BE)[tid] = ep;
+  }
+  chunk16 W[2][4];  // W1 register ring: unit u in set u % 2, loaded one unit ahead
+  wload(0, W[0]);
+  __syncthreads();
+
+  for (int j = tid; j < I_SVN; j += 512) {
+    const int r = j / NPOS2, i = j - r * NPOS2;
+    const int p = 4 * (t0 + i) - 2 + r;
+    const bool valid = i < GROWS2 && p >= 0 && p < L0;
+    float sm[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG2 - 1)];
+    float q = c0stat[C0Stat::BETA];
+#pragma unroll
+    for (int a = 0; a < 10; ++a) {
+      float ga = fmaf(c0stat[C0Stat::G + a * 10 + a], sm[a], 2.0f * c0stat[C0Stat::H + a]);
+#pragma unroll
+      for (int b = a + 1; b < 10; ++b) ga = fmaf(2.0f * c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
+      q = fmaf(ga, sm[a], q);
+    }
+    const float rs = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : 0.f;
+    bf16 hi[10], lo[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const float x = rs * sm[k];
+      hi[k] = (bf16)x;
+      lo[k] = (bf16)(x - (float)hi[k]);
+    }
+    const bf16 rb = (bf16)rs;
+    const bf16x8 v[4] = {{hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]},
+                         {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]},
+                         {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]},
+                         {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], rb, rb}};
+    unsigned char* row = SV + j * 64;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(bf16x8*)(row + sphys(j, c) * 16) = v[c];
+  }
+
+  // validity of this lane's position in slice tile x (pq + 4x, x < 4; 16 for x = 4) of phase r: bit 5r + x
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      const int pt = x == 4 ? 16 : pq + 4 * x;
+      const int p = 4 * (t0 + pt * 16 + (lane & 15)) - 2 + r;
+      vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
+    }
+  __syncthreads();
+
+  // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; this wave makes channel tile ct
+  auto read_c0 = [&](int v, chunk16& c0, f32x4& bt) {
+    const int g = v & 7;
+    c0 = ((const chunk16*)C0)[((2 * g + ct) * 16 + (lane & 15)) * 4 + (lane >> 4)];
+    bt = *(const f32x4*)(BE + (2 * g + ct) * 16 + 4 * (lane >> 4));
+  };
+  auto read_sv = [&](int v, int x) -> chunk16 {
+    const int pt = x == 4 ? 16 : pq + 4 * x;
+    const int jj = ((v >> 3) & 3) * NPOS2 + pt * 16 + (lane & 15);
+    return *(const chunk16*)(SV + jj * 64 + sphys(jj, lane >> 4) * 16);
+  };
+  auto pstore = [&](auto slc, int v, int x, const f32x4& z) {
+    const int pt = x == 4 ? 16 : pq + 4 * x;
+    const int prow = pt * 16 + (lane & 15);
+    const uint32_t m = 0u - ((vmask >> (5 * ((v >> 3) & 3) + x)) & 1u);
+    unsigned char* gs = G + decltype(slc)::value * I_GSLOT;
+    const u32x2 o = {relu_bf16x2(z[0], z[1]) & m, relu_bf16x2(z[2], z[3]) & m};
+    const int lc = 2 * ct + (lane >> 5);
+    *(u32x2*)(gs + prow * 64 + gphys(prow, lc) * 16 + ((lane >> 4) & 1) * 8) = o;
+  };
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {  // slices 0 and 1
+    chunk16 c0;
+    f32x4 bt;
+    read_c0(v, c0, bt);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      if (x == 4 && !p16) break;
+      const chunk16 sv = read_sv(v, x);
+      if (v == 0) pstore(std::integral_constant<int, 0>{}, v, x, mfma_chunk<bf16>(c0, sv, bt));
+      else pstore(std::integral_constant<int, 1>{}, v, x, mfma_chunk<bf16>(c0, sv, bt));
+    }
+  }
+
+  f32x16 acc[8];  // [row tile] of C^T (32 channels x 32 rows), in AGPRs
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  // fragment n = 16h + 8kh + i: tap offset h, k half kh (chunks 2kh + lane/32), row tile i
+  auto gread = [&](auto slc, int n) -> chunk16 {
+    const unsigned char* gs = G + decltype(slc)::value * I_GSLOT;
+    const int row = (n & 7) * 32 + (lane & 31) + (n >> 4);
+    return *(const chunk16*)(gs + row * 64 + gphys(row, 2 * ((n >> 3) & 1) + (lane >> 5)) * 16);
+  };
+  constexpr int GA = 3;  // G fragments in flight ahead of their MFMA (the ring, GA + 1, must divide 32)
+  chunk16 gf[GA + 1];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // slices 0, 1 published; WV (slot 2) free
+#pragma unroll
+  for (int n = 0; n < GA; ++n) gf[n] = gread(std::integral_constant<int, 0>{}, n);
+  stamp();
+
+  // unit u (slot u % 3 = SL, a compile-time constant so every LDS offset is an immediate)
+  auto unit = [&](const int u, auto slc, chunk16* wf, chunk16* wn1, const bool last1) {
+    constexpr int SL = decltype(slc)::value;
+    // B_u: own slice u+1 stores retired; W1 of unit u (issued one unit ago) landed
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (!last1) wload(u + 1, wn1);
+    const int v = u + 2;
+    chunk16 c0, sv;
+    f32x4 bt, z;
+    read_c0(v, c0, bt);
+#pragma unroll
+    for (int n = 0; n < 32; ++n) {
+      __builtin_amdgcn_sched_barrier(0);
+      // slice v: tile x operands at MFMA 7x, conv0 MFMA at 7x+2, store at 7x+4 (tile 16: 28 / 30 / 31)
+      if (n % 7 == 0 && n / 7 < 4) sv = read_sv(v, n / 7);
+      if (n % 7 == 2 && n / 7 < 4) z = mfma_chunk<bf16>(c0, sv, bt);
+      if (n % 7 == 4 && n / 7 < 4) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, n / 7, z);
+      if (p16) {
+        if (n == 28) sv = read_sv(v, 4);
+        if (n == 30) z = mfma_chunk<bf16>(c0, sv, bt);
+        if (n == 31) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, 4, z);
+      }
+      mfma32_acc(acc[n & 7], wf[n >> 3], gf[n % (GA + 1)]);
+      if (n + GA < 32) gf[(n + GA) % (GA + 1)] = gread(slc, n + GA);
+      else if (!last1) gf[(n + GA) % (GA + 1)] = gread(std::integral_constant<int, (SL + 1) % 3>{}, n + GA - 32);
+    }
+    if ((u & 7) == 7) stamp();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  for (int u = 0; u < 30; u += 6) {
+    unit(u, I0{}, W[0], W[1], false);
+    unit(u + 1, I1{}, W[1], W[0], false);
+    unit(u + 2, I2{}, W[0], W[1], false);
+    unit(u + 3, I0{}, W[1], W[0], false);
+    unit(u + 4, I1{}, W[0], W[1], false);
+    unit(u + 5, I2{}, W[1], W[0], false);
+  }
+  unit(30, I0{}, W[0], W[1], false);
+  unit(31, I1{}, W[1], W[0], true);
+
+  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[m = i*32 + lane%32][n = 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15
+#pragma unroll
+  for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live)
+  const int cb = w * 32 + 4 * (lane >> 5);  // channel of e = 0; e -> cb + 8(e/4) + e%4
+  f32x4 bb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(EP + cb + 8 * q);
+  auto val = [&](int i, int q) -> f32x4 {
+    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]} + bb[q];
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
+    float sum = (t[0] + t[1]) + (t[2] + t[3]);
+    sum += __shfl_xor(sum, 32, 64);
+    if (lane < 32) red[(i * 32 + lane) * 8 + w] = sum;
+  }
+  __syncthreads();
+  float mean[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
+    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
+    mean[i] = ((pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]))) * (1.0f / BN);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 d = val(i, q) - mean[i];
+      t += d * d;
+    }
+    float ss = (t[0] + t[1]) + (t[2] + t[3]);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 32) red[(i * 32 + lane) * 8 + w] = ss;
+  }
+  __syncthreads();
+  f32x4 gg[4], ee[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    gg[q] = *(const f32x4*)(EP + 256 + cb + 8 * q);
+    ee[q] = *(const f32x4*)(EP + 512 + cb + 8 * q);
+  }
+  // 16-B stores: for channel blocks (2p, 2p+1) one v_permlane32_swap per dword gives lanes 0-31 the
+  // 8 channels of block 2p and lanes 32-63 those of block 2p+1
+  bf16* obase = out + (int64_t)s * out_seq_stride;
+  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
+    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
+    const float var = (pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
+    const float rstd = rsqrtf(var * (1.0f / (BN - 1)) + 1e-5f);
+    const int t = t0 + i * 32 + (lane & 31);
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = (val(i, q) - mean[i]) * rstd * gg[q] + ee[q];
+      pk[q][0] = relu_bf16x2(v[0], v[1]);
+      pk[q][1] = relu_bf16x2(v[2], v[3]);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+        pk[2 * p][d] = sw[0];
+        pk[2 * p + 1][d] = sw[1];
+      }
+      const int col = w * 32 + 8 * (2 * p + (lane >> 5));
+      const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+      buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
+    }
+  }
+  if constexpr (STAMPS) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+    if (samp >= 0 && tid == 0)
+      for (int k = 0; k < 8 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, const bf16* c0w, const float* c0stat,
@@ -1058,7 +1385,17 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
     return hipGetLastError();
   }
   dim3 grid((r1 - r0 + BM2 - 1) / BM2, S);
-  static const bool v9 = getenv("VAP_CONV01_V9") != nullptr;  // the four-wave kernel (previous default)
+  static const bool v9 = getenv("VAP_CONV01_V9") != nullptr;    // the four-wave kernel
+  static const bool v10 = getenv("VAP_CONV01_V10") != nullptr;  // eight waves, 16x16x32 conv1 MFMAs
+  if (!v9 && !v10) {
+    if (stamps)
+      hipLaunchKernelGGL(conv01m_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
+                         b1, g1, be1, out, out_seq_stride, r0, r1);
+    else
+      hipLaunchKernelGGL(conv01m_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
+                         W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
+    return hipGetLastError();
+  }
   if (!v9) {
     if (stamps)
       hipLaunchKernelGGL(conv01k_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
