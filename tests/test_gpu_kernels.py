@@ -105,6 +105,40 @@ def test_gemm(prec, case):
     assert err <= tol * max(1.0, scale), f"{prec}/{case}: max err {err} (scale {scale})"
 
 
+@pytest.mark.parametrize("S,L_in,a,b", [(3, 160, 0, -1), (2, 1601, 0, -1), (2, 1600, 37, 301), (1, 514, 1, 257),
+                                         (4, 6000, 1000, -1)])
+def test_convk4(S, L_in, a, b):
+    """CPC conv2..4 kernel (k_conv234.hip): k4 s2 p1 conv + bias + ChannelNorm (unbiased) + ReLU on a
+    padded [S][L_in + 2][256] bf16 activation (one zero pad row in front and behind), output rows
+    [a, b) of the layer, against torch conv1d on the same bf16 inputs (encoder_components.py:87-103)."""
+    N = lib()
+    g = torch.Generator().manual_seed(7)
+    L_out = (L_in + 2 - 4) // 2 + 1
+    b = L_out if b < 0 else b
+    M = b - a
+    x = torch.relu(torch.randn(S, L_in, 256, generator=g)).to(torch.bfloat16)
+    W = (torch.randn(256, 256, 4, generator=g) / 32).to(torch.bfloat16)  # [out][in][tap]
+    bias = torch.randn(256, generator=g) * 0.1
+    gamma = 1 + 0.2 * torch.randn(256, generator=g)
+    beta = 0.1 * torch.randn(256, generator=g)
+    ref = F.conv1d(x.float().transpose(1, 2), W.float(), bias, stride=2, padding=1).transpose(1, 2)[:, a:b]
+    mu, var = ref.mean(-1, keepdim=True), ref.var(-1, keepdim=True)
+    ref = torch.relu((ref - mu) * torch.rsqrt(var + 1e-5) * gamma + beta)
+    xp = torch.zeros(S, L_in + 2, 256, dtype=torch.bfloat16)
+    xp[:, 1:L_in + 1] = x
+    xd = xp.cuda()
+    wpk = W.permute(0, 2, 1).reshape(256, 1024).contiguous().cuda()  # [n][tap * 256 + ci]
+    out = torch.full((S, M + 3, 256), 7.0, dtype=torch.bfloat16, device="cuda")
+    in_off = 2 * a * 256 * 2
+    bd, gd, bed = bias.cuda(), gamma.cuda(), beta.cuda()  # named: temporaries would be freed and reused
+    _run(N.lib().vap_test_convk4, xd.data_ptr() + in_off, (L_in + 2) * 256, L_in + 2 - 2 * a, _p(wpk),
+         _p(bd), _p(gd), _p(bed), _p(out), (M + 3) * 256, M, S, _st())
+    got = out.float().cpu()
+    err = (got[:, :M] - ref).abs().max().item()
+    assert err <= 3e-2 * max(1.0, ref.abs().max().item()), f"max err {err}"
+    assert torch.all(got[:, M:] == 7.0), "rows past the range were written"
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("kv_swap", [0, 1])
 def test_attention(prec, kv_swap):

@@ -1,0 +1,282 @@
+// CPC conv2 / conv3 / conv4 (256 -> 256, k=4, s=2, p=1) + bias + ChannelNorm + ReLU, bf16 perf mode.
+//
+// Reference: CPCEncoder conv2..conv4 + batchNorm2..4 (vap/encoder_components.py:87-92, 101-103),
+// ChannelNorm (:62-70, unbiased variance over the 256 channels).
+//
+// Output row t of a layer reads input rows 2t-1 .. 2t+2 (tap j -> row 2t-1+j; the activation
+// buffers carry one zero pad row in front, so buffer row 2t+j).  gemm2 staged every tap's A rows
+// separately (each input row reached LDS twice) and its W tiles by LDS-DMA: four DMA pieces per
+// wave and k-step, whose issue cost (~100 cycles each beside MFMAs) serialised with the MFMA issue.
+// Here, per 256-row output tile and 32-channel input block cb:
+//   * the block's input slab (buffer rows 2t0 .. 2t0+513) is staged ONCE by LDS-DMA, even and odd
+//     rows in separate halves: tap j of output row t is row t + j/2 of half j%2, so the four taps
+//     read 32 CONSECUTIVE half-rows (conflict-free with the chunk' = chunk + row/4 swizzle) instead
+//     of stride-2 rows;  34 pieces of 1 KiB per block for 4 k-steps (gemm2: 128; six are issued
+//     twice so that every wave issues five);
+//   * W (k-step-major [tap*8 + cb][256][32], launch_pack_kstep) goes from L2 straight into
+//     registers: wave w owns output channels 32w .. 32w+31, so no two waves share a fragment;
+//   * 8 waves (two per SIMD), 8 row tiles of 32 x one 32-channel tile per wave on
+//     v_mfma_f32_32x32x16_bf16 (128 accumulators in AGPRs);
+//   * slabs rotate through 3 LDS slots, two blocks ahead; one barrier per block (4 k-steps);
+//   * epilogue: bias, ChannelNorm over 8 per-wave partials through LDS, ReLU, 16-B bf16 stores
+//     assembled with v_permlane32_swap.
+#include <type_traits>
+
+#include "vap_common.h"
+#include "vap_kernels.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int CK_HR = 272;                 // rows per parity half (>= 257: 256 outputs + the tap-2/3 row)
+constexpr int CK_HALF = CK_HR * 64;        // 17408 B
+constexpr int CK_SLAB = 2 * CK_HALF;       // 34816 B
+constexpr int CK_LDS = 3 * CK_SLAB;        // 104448 B
+constexpr int CK_PIECES = 2 * (CK_HR / 16);  // 34 DMA pieces of 16 half-rows x 64 B per slab
+
+VAP_DEV int ck_phys(int row, int c) { return (c + (row >> 2)) & 3; }
+VAP_DEV void ck_mfma(f32x16& c, const chunk16& a, const chunk16& b) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+VAP_DEV uint32_t ck_relu2(float a, float b) {  // bf16(max(x, 0)) for two values
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2_t h = __builtin_convertvector((f32x2){a, b}, bf16x2_t);
+  s16x2 v = __builtin_bit_cast(s16x2, h);
+  v = __builtin_elementwise_max(v, (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int DBG>
+__global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[CK_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32w .. 32w+31
+  const int s = blockIdx.y;
+  const int t0 = blockIdx.x * 256;
+  const bf16* in = a.in + (int64_t)s * a.in_seq_stride;
+
+  // ---- DMA of input block cb (channels 32cb..) into slot sl: pieces q = w + 8k (34 per slab)
+  // Every wave issues 5 pieces (waves 2..7 repeat their 4th: the same bytes to the same place), so
+  // the DMA count per wave is uniform and the compiler can count vmcnt past it (a branch around the
+  // 5th piece made it fall back to vmcnt(0) before each block's first MFMA).
+  auto piece = [&](int k) { return k == 4 && w >= 2 ? w + 24 : w + 8 * k; };
+  uint32_t dsrc[5];               // element offsets (channel block 0) of this lane's source per piece
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int q = piece(k);
+    const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
+    const int hr = 16 * p + (lane >> 2);
+    const int c = ((lane & 3) - (hr >> 2)) & 3;  // logical chunk held at physical chunk lane%4
+    const int row = min(2 * t0 + 2 * hr + hb, a.in_rows - 1);  // rows past the range feed no stored output
+    dsrc[k] = (uint32_t)(row * 256 + c * 8);
+  }
+  // Both the slab DMA and the W loads are inline asm with hand-counted waits: the compiler treats a
+  // global_load_lds as an LDS write that may alias every later ds_read and put vmcnt(0) before each
+  // block's first MFMA, draining the two-block-deep DMA stream.  Per block the wave issues, in order,
+  // W(CB+1) (8 loads) then DMA(CB+2) (5 pieces); at the start of block CB, vmcnt(5) leaves only
+  // DMA(CB+1) in flight, so W(CB) and DMA(CB) have landed.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  auto dma = [&](int cb, int sl) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int q = piece(k);
+      const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
+      const bf16* src = in + dsrc[k] + cb * 32;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(sl * CK_SLAB + hb * CK_HALF + p * 1024));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  };
+  // ---- W fragments of block cb: [tap j][k half kh] (A of the 32x32x16: channel 32w + lane%32)
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.W, 32 * 256 * 64);
+  const uint32_t wlo = (uint32_t)((w * 32 + (lane & 31)) * 64 + (lane >> 5) * 16);
+  auto wload = [&](int cb, chunk16* wf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(wf[j * 2 + kh])
+                     : "v"(wlo), "s"(wrs), "s"((j * 8 + cb) * 16384 + kh * 32) : "memory");
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  // zero the accumulators HERE, with the wait states an MFMA reading them as SrcC needs after the
+  // v_accvgpr writes (the MFMAs are inline asm, invisible to the compiler's hazard recognizer;
+  // left alone it sank each tile's zeroing to just before its first MFMA)
+  asm volatile("s_nop 4" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+  asm volatile("s_nop 4" : "+a"(acc[4]), "+a"(acc[5]), "+a"(acc[6]), "+a"(acc[7]));
+
+  chunk16 W[2][8];
+  wload(0, W[0]);
+  dma(0, 0);
+  dma(1, 1);
+
+  // G fragment (tap j, k half kh, row tile i) -> half j%2, rows 32i + lane%32 + j/2.  The swizzle
+  // depends on the lane, j/2 and kh only (32i is a multiple of 4 rows), so a block reads through four
+  // lane bases (+ the slot, set per block) and immediate offsets (half, row tile)
+  uint32_t gbase0[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int jh = v >> 1, kh = v & 1;
+    const int row = (lane & 31) + jh;
+    gbase0[v] = (uint32_t)(row * 64 + ck_phys(row, 2 * kh + (lane >> 5)) * 16);
+  }
+  auto block = [&](auto cbc, chunk16* wf, chunk16* wn) {
+    constexpr int CB = decltype(cbc)::value, SL = CB % 3;
+    uint32_t gb[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      gb[v] = gbase0[v] + SL * CK_SLAB;
+      asm volatile("" : "+v"(gb[v]));  // materialised here, not hoisted out of the blocks
+    }
+    auto gread = [&](int sl, int j, int kh, int i) -> chunk16 {
+      (void)sl;
+      return *(const chunk16*)(smem + gb[(j >> 1) * 2 + kh] + (j & 1) * CK_HALF + i * 2048);
+    };
+    // own DMA of block CB and W of CB landed (younger: only block CB+1's DMA pieces)
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (CB + 1 < 8) {
+      asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of CB landed; slot (CB+2)%3 fully read
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (CB + 1 < 8) wload(CB + 1, wn);
+    if constexpr (CB + 2 < 8) dma(CB + 2, (CB + 2) % 3);
+    constexpr int GA = 3;
+    chunk16 gf[GA + 1];
+#pragma unroll
+    for (int n = 0; n < GA; ++n) gf[n] = gread(SL, n >> 4, (n >> 3) & 1, n & 7);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {  // n = 16j + 8kh + i
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((DBG & 6) != 0) {
+        const chunk16 one = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+        ck_mfma(acc[n & 7], (DBG & 4) ? one : wf[n >> 3], (DBG & 2) ? one : gf[n & GA]);
+      } else {
+        ck_mfma(acc[n & 7], wf[n >> 3], gf[n & GA]);
+      }
+      const int m = n + GA;
+      if (m < 64) gf[m & GA] = gread(SL, m >> 4, (m >> 3) & 1, m & 7);
+    }
+  };
+  block(std::integral_constant<int, 0>{}, W[0], W[1]);
+  block(std::integral_constant<int, 1>{}, W[1], W[0]);
+  block(std::integral_constant<int, 2>{}, W[0], W[1]);
+  block(std::integral_constant<int, 3>{}, W[1], W[0]);
+  block(std::integral_constant<int, 4>{}, W[0], W[1]);
+  block(std::integral_constant<int, 5>{}, W[1], W[0]);
+  block(std::integral_constant<int, 6>{}, W[0], W[1]);
+  block(std::integral_constant<int, 7>{}, W[1], W[0]);
+
+  // ---------------- epilogue: + bias, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[row = i*32 + lane%32][channel 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15
+#pragma unroll
+  for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done reading the slabs: red overlaps slot 0
+  float* red = (float*)smem;     // [256 rows][8 waves]
+  const int cb0 = w * 32 + 4 * (lane >> 5);
+  f32x4 bb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(a.bias + cb0 + 8 * q);
+  auto val = [&](int i, int q) -> f32x4 {
+    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]} + bb[q];
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
+    float sum = (t[0] + t[1]) + (t[2] + t[3]);
+    sum += __shfl_xor(sum, 32, 64);
+    if (lane < 32) red[(i * 32 + lane) * 8 + w] = sum;
+  }
+  __syncthreads();
+  auto rowsum = [&](int i) -> float {
+    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
+    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
+    return ((pa[0] + pa[1]) + (pa[2] + pa[3])) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
+  };
+  float mean[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mean[i] = rowsum(i) * (1.0f / 256);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 d = val(i, q) - mean[i];
+      t += d * d;
+    }
+    float ss = (t[0] + t[1]) + (t[2] + t[3]);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 32) red[(i * 32 + lane) * 8 + w] = ss;
+  }
+  __syncthreads();
+  f32x4 gg[4], ee[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    gg[q] = *(const f32x4*)(a.gamma + cb0 + 8 * q);
+    ee[q] = *(const f32x4*)(a.beta + cb0 + 8 * q);
+  }
+  bf16* obase = a.out + (int64_t)s * a.out_seq_stride;
+  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)a.M * 256 * 2));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float rstd = rsqrtf(rowsum(i) * (1.0f / 255) + 1e-5f);
+    const int t = t0 + i * 32 + (lane & 31);
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - mean[i]) * rstd * gg[q] + ee[q];
+      if constexpr ((DBG & 1) != 0) {
+        pk[q][0] = pack_bf16x4(v[0], v[1], v[2], v[3])[0];
+        pk[q][1] = pack_bf16x4(v[0], v[1], v[2], v[3])[1];
+      } else {
+        pk[q][0] = ck_relu2(v[0], v[1]);
+        pk[q][1] = ck_relu2(v[2], v[3]);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+        pk[2 * p][d] = sw[0];
+        pk[2 * p + 1][d] = sw[1];
+      }
+      const int col = w * 32 + 8 * (2 * p + (lane >> 5));
+      const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+      buf_store16(orsc, t < a.M ? (uint32_t)((t * 256 + col) * 2) : 0xFFFFFFF0u, o);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
+  if (S <= 0 || a.M <= 0 || a.in_rows < 2 * a.M + 2) return hipErrorInvalidValue;
+  if (a.in_seq_stride % 8 || a.out_seq_stride % 8)
+    return hipErrorInvalidValue;
+  if ((int64_t)a.M * 256 * 2 >= (1ll << 32) || (int64_t)a.in_rows * 256 >= (1ll << 31)) return hipErrorInvalidValue;
+  const dim3 grid((a.M + 255) / 256, S);
+  switch (a.dbg) {
+    case 0: hipLaunchKernelGGL(convk4_kernel<0>, grid, dim3(512), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(convk4_kernel<1>, grid, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(convk4_kernel<3>, grid, dim3(512), 0, st, a); break;
+    case 5: hipLaunchKernelGGL(convk4_kernel<5>, grid, dim3(512), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

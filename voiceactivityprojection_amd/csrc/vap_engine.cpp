@@ -85,6 +85,8 @@ struct vap_handle {
   // recurrence split over workgroup pairs (k_lstm.hip lstm_pair_kernel; VAP_LSTM_PAIR=0: one CU per
   // 16 sequences, lstm_resident_kernel): its exchange buffer and launch epoch (exchange tags)
   bool lstm_pair = true;
+  // conv2..4 on the slab-staged k4 s2 kernel (k_conv234.hip); VAP_CONVK4=0: implicit GEMMs on gemm2
+  bool convk4 = true;
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
   unsigned xepoch = 0;
@@ -457,10 +459,13 @@ int pack_all(vap_handle* h, hipStream_t st) {
     if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv");
     HIPCHK(launch_pack_conv<T>(h->P(g + ".conv" + std::to_string(i) + ".weight"), w, D, D, kws[i], st));
   }
-  if constexpr (sizeof(T) == 2) {  // conv1 in the k-step-major layout of conv01's W1 stages
-    T* w = alloc("conv1_ks", (int64_t)D * D * kws[1]);
-    if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv1");
-    HIPCHK(launch_pack_kstep((const bf16*)h->W<T>("conv1"), (bf16*)w, D, D * kws[1], st));
+  if constexpr (sizeof(T) == 2) {  // conv1..4 in the k-step-major layout (conv01's W1 stages, convk4's W)
+    for (int i = 1; i < 5; ++i) {
+      const std::string c = "conv" + std::to_string(i);
+      T* w = alloc(c + "_ks", (int64_t)D * D * kws[i]);
+      if (!w) return fail(VAP_ERR_HIP, "hipMalloc packed conv (k-step major)");
+      HIPCHK(launch_pack_kstep((const bf16*)h->W<T>(c), (bf16*)w, D, D * kws[i], st));
+    }
   }
   for (int l = 0; l < h->dims.lstm_layers; ++l) {
     const std::string p = "encoder.encoder.gAR.baseNet.", s = "_l" + std::to_string(l);
@@ -763,6 +768,15 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   for (int i = first; i < 4; ++i) {
     const std::string c = std::to_string(i + 1);
     Timed tm(h, i == 0 ? VAP_K_CONV1 : VAP_K_CONV234, st);
+    if constexpr (sizeof(T) == 2) {
+      if (i >= 1 && h->convk4) {
+        ConvK4Args ca{(const bf16*)ins[i], in_ss[i], (int)(in_ss[i] / D), (const bf16*)h->W<T>("conv" + c + "_ks"),
+                      h->P(g + ".conv" + c + ".bias"), h->P(g + ".batchNorm" + c + ".weight"),
+                      h->P(g + ".batchNorm" + c + ".bias"), (bf16*)(Xs[i] + D), ss[i], (int)L[i + 1]};
+        HIPCHK(launch_convk4(ca, S, st));
+        continue;
+      }
+    }
     GemmArgs ga = gargs(ins[i], lda[i], in_ss[i], h->W<T>("conv" + c), Ks[i], D, h->P(g + ".conv" + c + ".bias"),
                         (int)L[i + 1], S, Xs[i] + D, D, ss[i]);
     ga.norm = 1;
@@ -1319,6 +1333,13 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   for (int i = 1; i < 4; ++i) {  // conv2..4 (encoder_components.py:100-103)
     const std::string cs = std::to_string(i + 1);
     Timed tm(h, VAP_K_CONV234, st);
+    if (h->convk4) {
+      ConvK4Args ca{Xs[i - 1] + a[i] * 2 * D, ss[i - 1], (int)(ss[i - 1] / D - 2 * a[i]), (const bf16*)h->W<T>("conv" + cs + "_ks"),
+                    h->P(g + ".conv" + cs + ".bias"), h->P(g + ".batchNorm" + cs + ".weight"),
+                    h->P(g + ".batchNorm" + cs + ".bias"), Xs[i] + D + a[i] * D, ss[i], (int)(b[i] - a[i])};
+      HIPCHK(launch_convk4(ca, S, st));
+      continue;
+    }
     GemmArgs ga = gargs(Xs[i - 1] + a[i] * 2 * D, 2 * D, ss[i - 1], h->W<T>("conv" + cs), 4 * D, D,
                         h->P(g + ".conv" + cs + ".bias"), (int)(b[i] - a[i]), S, Xs[i] + D + a[i] * D, D, ss[i]);
     ga.norm = 1;
@@ -1791,6 +1812,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   if (const char* e = getenv("VAP_LSTM_PAIR")) h->lstm_pair = atoi(e) != 0;
+  if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;

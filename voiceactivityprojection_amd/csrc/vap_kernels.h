@@ -24,6 +24,25 @@ struct GemmArgs {
 
 template <typename T, typename TOut>
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+
+// bf16 CPC conv2..4 (k4 s2 p1, 256 -> 256) + bias + ChannelNorm + ReLU (k_conv234.hip).  `in` points at
+// the buffer row 2*a of the first output row a of the range (one zero pad row in front of each
+// sequence), in_rows = rows readable per sequence from there (>= 2M + 2); W in the k-step-major
+// layout [tap*8 + cb][256][32] (launch_pack_kstep of the [N][tap*256 + ci] packing); out = row a.
+struct ConvK4Args {
+  const bf16* in;
+  int64_t in_seq_stride;
+  int in_rows;
+  const bf16* W;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  bf16* out;
+  int64_t out_seq_stride;
+  int M;
+  int dbg = 0;  // diagnostics (tools/diag_convk4.py): 1 raw conv + bias out, 2 G := 1, 4 W := 1
+};
+hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st);
 // bf16 256x256-tile LDS-DMA variant (k_gemm2.hip); launch_gemm<bf16, *> dispatches to it
 template <typename TOut>
 hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st);

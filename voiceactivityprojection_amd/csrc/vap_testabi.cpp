@@ -3,6 +3,7 @@
 // engine itself.  precision: VAP_PRECISION_FP32 (storage float) / VAP_PRECISION_BF16 (storage bf16).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 
 #include "../../include/vap_hip.h"
@@ -59,6 +60,22 @@ int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, cons
   if (precision == VAP_PRECISION_BF16)
     return rc_of(out_f32 ? launch_gemm<bf16, float>(g, st) : launch_gemm<bf16, bf16>(g, st));
   return rc_of(launch_gemm<float, float>(g, st));
+}
+
+// CPC conv2..4 kernel (k_conv234.hip): W [256][1024] bf16 in the tap-major packing of the engine
+// ([n][tap*256 + ci]); repacked k-step major into a scratch buffer here
+int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, const float* bias, const float* gamma,
+                    const float* beta, void* out, int64_t out_seq, int M, int S, void* stream) {
+  static const int dbg = getenv("VAP_CONVK4_DBG") ? atoi(getenv("VAP_CONVK4_DBG")) : 0;
+  hipStream_t st = (hipStream_t)stream;
+  void* wks = nullptr;
+  if (hipMalloc(&wks, 256 * 1024 * 2) != hipSuccess) return VAP_ERR_HIP;
+  int rc = rc_of(launch_pack_kstep((const bf16*)W, (bf16*)wks, 256, 1024, st));
+  ConvK4Args a{(const bf16*)in, in_seq, in_rows, (const bf16*)wks, bias, gamma, beta, (bf16*)out, out_seq, M, dbg};
+  if (rc == VAP_OK) rc = rc_of(launch_convk4(a, S, st));
+  if (hipStreamSynchronize(st) != hipSuccess) rc = VAP_ERR_HIP;
+  hipFree(wks);
+  return rc;
 }
 
 int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq, const void* K, int64_t k_ld,
