@@ -90,6 +90,7 @@ _SIGS = {
                                          _P, _P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_probe_mfma_f32": (ctypes.c_int, [_P, _P, _P, _P]),
     "vap_test_convk4": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, _P, _P, _P, _P, _I64, ctypes.c_int, ctypes.c_int, _P]),
+    "vap_test_convk4_stamps": (ctypes.c_int, [_P]),
     "vap_last_error": (ctypes.c_char_p, []),
     "vap_build_info": (ctypes.c_char_p, []),
 }

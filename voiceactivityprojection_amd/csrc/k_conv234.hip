@@ -18,8 +18,9 @@
 //   * 8 waves (two per SIMD), 8 row tiles of 32 x one 32-channel tile per wave on
 //     v_mfma_f32_32x32x16_bf16 (128 accumulators in AGPRs);
 //   * slabs rotate through 3 LDS slots, two blocks ahead; one barrier per block (4 k-steps);
-//   * epilogue: bias, ChannelNorm over 8 per-wave partials through LDS, ReLU, 16-B bf16 stores
-//     assembled with v_permlane32_swap.
+//   * epilogue: the accumulators start at the bias; ChannelNorm from ONE exchange of per-wave
+//     (mean, M2) pairs over its 32 channels (Chan's parallel variance), gamma / beta from LDS, ReLU,
+//     16-B bf16 stores assembled with v_permlane32_swap.
 #include <type_traits>
 
 #include "vap_common.h"
@@ -33,7 +34,9 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int CK_HR = 272;                 // rows per parity half (>= 257: 256 outputs + the tap-2/3 row)
 constexpr int CK_HALF = CK_HR * 64;        // 17408 B
 constexpr int CK_SLAB = 2 * CK_HALF;       // 34816 B
-constexpr int CK_LDS = 3 * CK_SLAB;        // 104448 B
+constexpr int CK_RED = 3 * CK_SLAB;        // 104448: [256 rows][8 waves] (mean, M2) float2 (epilogue)
+constexpr int CK_PAR = CK_RED + 256 * 8 * 8;  // 120832: bias | gamma | beta, 3 x 256 fp32
+constexpr int CK_LDS = CK_PAR + 3 * 256 * 4;  // 123904 B
 constexpr int CK_PIECES = 2 * (CK_HR / 16);  // 34 DMA pieces of 16 half-rows x 64 B per slab
 
 VAP_DEV int ck_phys(int row, int c) { return (c + (row >> 2)) & 3; }
@@ -57,6 +60,21 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
   const int s = blockIdx.y;
   const int t0 = blockIdx.x * 256;
   const bf16* in = a.in + (int64_t)s * a.in_seq_stride;
+  unsigned long long stv[12];
+  int nst = 0;
+  auto stamp = [&]() {
+    if constexpr ((DBG & 16) != 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (nst < 12) stv[nst] = __builtin_amdgcn_s_memtime();
+      ++nst;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp();
+  if (tid < 192) {  // bias | gamma | beta -> LDS
+    const float* src = tid < 64 ? a.bias : (tid < 128 ? a.gamma : a.beta);
+    ((f32x4*)(smem + CK_PAR))[tid] = ((const f32x4*)src)[tid & 63];
+  }
 
   // ---- DMA of input block cb (channels 32cb..) into slot sl: pieces q = w + 8k (34 per slab)
   // Every wave issues 5 pieces (waves 2..7 repeat their 4th: the same bytes to the same place), so
@@ -103,12 +121,21 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
                      : "v"(wlo), "s"(wrs), "s"((j * 8 + cb) * 16384 + kh * 32) : "memory");
   };
 
+  // the accumulators start at the bias (lane element e: channel 32w + 8(e/4) + 4(lane/32) + e%4)
+  const int cb0 = w * 32 + 4 * (lane >> 5);
   f32x16 acc[8];
+  {
+    const float* PR = (const float*)(smem + CK_PAR);
+    __syncthreads();  // parameters in LDS
+    f32x4 bb[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(PR + cb0 + 8 * q);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-  // zero the accumulators HERE, with the wait states an MFMA reading them as SrcC needs after the
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = bb[e >> 2][e & 3];
+  }
+  // write the accumulators HERE, with the wait states an MFMA reading them as SrcC needs after the
   // v_accvgpr writes (the MFMAs are inline asm, invisible to the compiler's hazard recognizer;
   // left alone it sank each tile's zeroing to just before its first MFMA)
   asm volatile("s_nop 4" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
@@ -150,6 +177,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
     }
     __builtin_amdgcn_s_barrier();  // every wave's pieces of CB landed; slot (CB+2)%3 fully read
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
     if constexpr (CB + 1 < 8) wload(CB + 1, wn);
     if constexpr (CB + 2 < 8) dma(CB + 2, (CB + 2) % 3);
     constexpr int GA = 3;
@@ -178,68 +206,54 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
   block(std::integral_constant<int, 6>{}, W[0], W[1]);
   block(std::integral_constant<int, 7>{}, W[1], W[0]);
 
-  // ---------------- epilogue: + bias, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[row = i*32 + lane%32][channel 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15
+  stamp();
+  // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[row = i*32 + lane%32][channel 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15 (+ bias)
 #pragma unroll
   for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
                  : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done reading the slabs: red overlaps slot 0
-  float* red = (float*)smem;     // [256 rows][8 waves]
-  const int cb0 = w * 32 + 4 * (lane >> 5);
-  f32x4 bb[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(a.bias + cb0 + 8 * q);
+  const float* PR = (const float*)(smem + CK_PAR);
+  float2* red = (float2*)(smem + CK_RED);  // [256 rows][8 waves] (mean, M2) of the wave's 32 channels
   auto val = [&](int i, int q) -> f32x4 {
-    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]} + bb[q];
+    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
   };
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
     float sum = (t[0] + t[1]) + (t[2] + t[3]);
     sum += __shfl_xor(sum, 32, 64);
-    if (lane < 32) red[(i * 32 + lane) * 8 + w] = sum;
-  }
-  __syncthreads();
-  auto rowsum = [&](int i) -> float {
-    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
-    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
-    return ((pa[0] + pa[1]) + (pa[2] + pa[3])) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
-  };
-  float mean[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) mean[i] = rowsum(i) * (1.0f / 256);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    const float mw = sum * (1.0f / 32);
+    f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 d = val(i, q) - mean[i];
-      t += d * d;
+      const f32x4 d = val(i, q) - mw;
+      d2 += d * d;
     }
-    float ss = (t[0] + t[1]) + (t[2] + t[3]);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 32) red[(i * 32 + lane) * 8 + w] = ss;
+    float m2 = (d2[0] + d2[1]) + (d2[2] + d2[3]);
+    m2 += __shfl_xor(m2, 32, 64);
+    if (lane < 32) red[(i * 32 + lane) * 8 + w] = float2{mw, m2};
   }
   __syncthreads();
-  f32x4 gg[4], ee[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    gg[q] = *(const f32x4*)(a.gamma + cb0 + 8 * q);
-    ee[q] = *(const f32x4*)(a.beta + cb0 + 8 * q);
-  }
   bf16* obase = a.out + (int64_t)s * a.out_seq_stride;
   const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)a.M * 256 * 2));
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    float rstd = rsqrtf(rowsum(i) * (1.0f / 255) + 1e-5f);
+    // Chan: 8 groups of 32 channels: mean = mean of the group means, M2 = sum M2_w + 32 sum (m_w - m)^2
+    const f32x4* rp = (const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
+    const f32x4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+    const float m = (((r0[0] + r0[2]) + (r1[0] + r1[2])) + ((r2[0] + r2[2]) + (r3[0] + r3[2]))) * 0.125f;
+    auto dev = [&](float mw) { return (mw - m) * (mw - m); };
+    const float M2 = (((r0[1] + r0[3]) + (r1[1] + r1[3])) + ((r2[1] + r2[3]) + (r3[1] + r3[3]))) +
+                     32.0f * (((dev(r0[0]) + dev(r0[2])) + (dev(r1[0]) + dev(r1[2]))) +
+                              ((dev(r2[0]) + dev(r2[2])) + (dev(r3[0]) + dev(r3[2]))));
+    const float rstd = rsqrtf(M2 * (1.0f / 255) + 1e-5f);
     const int t = t0 + i * 32 + (lane & 31);
     uint32_t pk[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - mean[i]) * rstd * gg[q] + ee[q];
+      const f32x4 gg = *(const f32x4*)(PR + 256 + cb0 + 8 * q), ee = *(const f32x4*)(PR + 512 + cb0 + 8 * q);
+      const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - m) * rstd * gg + ee;
       if constexpr ((DBG & 1) != 0) {
         pk[q][0] = pack_bf16x4(v[0], v[1], v[2], v[3])[0];
         pk[q][1] = pack_bf16x4(v[0], v[1], v[2], v[3])[1];
@@ -261,6 +275,13 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
       buf_store16(orsc, t < a.M ? (uint32_t)((t * 256 + col) * 2) : 0xFFFFFFF0u, o);
     }
   }
+  if constexpr ((DBG & 16) != 0) {
+    stamp();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+    if (s == 0 && blockIdx.x < 8 && tid == 0)
+      for (int k = 0; k < 12; ++k) a.stamps[blockIdx.x * 12 + k] = stv[k];
+  }
 }
 
 }  // namespace
@@ -276,6 +297,7 @@ hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
     case 1: hipLaunchKernelGGL(convk4_kernel<1>, grid, dim3(512), 0, st, a); break;
     case 3: hipLaunchKernelGGL(convk4_kernel<3>, grid, dim3(512), 0, st, a); break;
     case 5: hipLaunchKernelGGL(convk4_kernel<5>, grid, dim3(512), 0, st, a); break;
+    case 16: hipLaunchKernelGGL(convk4_kernel<16>, grid, dim3(512), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

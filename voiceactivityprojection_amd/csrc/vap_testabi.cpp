@@ -64,6 +64,11 @@ int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, cons
 
 // CPC conv2..4 kernel (k_conv234.hip): W [256][1024] bf16 in the tap-major packing of the engine
 // ([n][tap*256 + ci]); repacked k-step major into a scratch buffer here
+static unsigned long long* stamps_out = nullptr;  // host buffer for VAP_CONVK4_DBG=16 (vap_test_convk4_stamps)
+int vap_test_convk4_stamps(unsigned long long* host) {
+  stamps_out = host;
+  return VAP_OK;
+}
 int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, const float* bias, const float* gamma,
                     const float* beta, void* out, int64_t out_seq, int M, int S, void* stream) {
   static const int dbg = getenv("VAP_CONVK4_DBG") ? atoi(getenv("VAP_CONVK4_DBG")) : 0;
@@ -71,10 +76,13 @@ int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, 
   void* wks = nullptr;
   if (hipMalloc(&wks, 256 * 1024 * 2) != hipSuccess) return VAP_ERR_HIP;
   int rc = rc_of(launch_pack_kstep((const bf16*)W, (bf16*)wks, 256, 1024, st));
-  ConvK4Args a{(const bf16*)in, in_seq, in_rows, (const bf16*)wks, bias, gamma, beta, (bf16*)out, out_seq, M, dbg};
+  static unsigned long long* stamps = nullptr;
+  if (dbg & 16 && !stamps && hipMalloc(&stamps, 8 * 12 * 8) != hipSuccess) return VAP_ERR_HIP;
+  ConvK4Args a{(const bf16*)in, in_seq, in_rows, (const bf16*)wks, bias, gamma, beta, (bf16*)out, out_seq, M, dbg, stamps};
   if (rc == VAP_OK) rc = rc_of(launch_convk4(a, S, st));
   if (hipStreamSynchronize(st) != hipSuccess) rc = VAP_ERR_HIP;
   hipFree(wks);
+  if (dbg & 16 && stamps_out && hipMemcpy(stamps_out, stamps, 8 * 12 * 8, hipMemcpyDeviceToHost) != hipSuccess) rc = VAP_ERR_HIP;
   return rc;
 }
 
