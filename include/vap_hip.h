@@ -228,6 +228,13 @@ int vap_test_read_rp_stamps(unsigned long long* out);
 int vap_test_read_ffn_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 2 x 4 x 6 s_memtime stamps of sampled bf16 GEMM k-steps (VAP_GEMM2_STAMPS=1) */
 int vap_test_read_gemm_stamps(unsigned long long* out);  /* + 8 x 6 tile-phase stamps after the 8 x 2 x 4 x 6 */
+/* CPC conv2..4 slab kernel (k_conv234.hip) on its own: conv k4 s2 256->256 + bias + ChannelNorm + ReLU.
+ * in: bf16 rows [S][in_seq] with one zero pad row in front (output t reads buffer rows 2t .. 2t+3), in_rows
+ * readable; W [256][1024] bf16 in the engine's tap-major packing ([n][tap*256 + ci]); out rows [S][out_seq], M per sequence */
+int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, const float* bias, const float* gamma,
+                    const float* beta, void* out, int64_t out_seq, int M, int S, void* stream);
+/* timing diagnostics: host buffer that receives 8 x 12 phase stamps of the next vap_test_convk4 (VAP_CONVK4_DBG=16) */
+int vap_test_convk4_stamps(unsigned long long* host);
 /* timing diagnostics: 8 x 4 x 5 s_memtime stamps of bf16 LSTM steps 100..103 (VAP_LSTM_STAMPS=1) */
 int vap_test_read_lstm_stamps(unsigned long long* out);
 
