@@ -237,6 +237,10 @@ int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, 
 int vap_test_convk4_stamps(unsigned long long* host);
 /* timing diagnostics: 8 x 4 x 5 s_memtime stamps of bf16 LSTM steps 100..103 (VAP_LSTM_STAMPS=1) */
 int vap_test_read_lstm_stamps(unsigned long long* out);
+/* timing diagnostics (VAP_LSTM_HANDOFF=1): s_memrealtime (100 MHz) of the last pair recurrence's workgroup 0:
+ * out[0] launch start, then per time chunk c: out[1+3c] ready wait begins, out[2+3c] ready seen,
+ * out[3+3c] done published (49 values) */
+int vap_test_read_lstm_handoff(unsigned long long* out);
 
 #ifdef __cplusplus
 }

@@ -437,6 +437,8 @@ VAP_DEV u32x4 xload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);  // sc1: L2-coherent, bypasses L1
 }
 
+__device__ unsigned long long g_lstm_handoff[1 + 3 * 16];
+
 template <bool PRE, bool ST>
 __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restrict__ gx, int S, int Tn,
                                                           const chunk16* __restrict__ wp, bf16* __restrict__ out,
@@ -451,6 +453,11 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   const bool valid = seq < S;
   const int u0 = 128 * p + 16 * w + 4 * (lane >> 4);  // this lane's 4 units (rows of the gate tiles)
 
+  if (sync.wave_prio && w < 4) {  // the two waves of a SIMD (w, w + 4) out of step: w's cells beside w+4's MFMAs
+    if (sync.wave_prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (sync.wave_prio == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  }
   chunk16 wa[P_NF];  // fragment f = g*8 + kk: rows g*256 + 128p + 16w + (lane&15), k = 32kk + 8(lane>>4) + e
   const chunk16* wsrc = wp + (int64_t)(p * P_NW + w) * P_NF * 64 + lane;
 #pragma unroll
@@ -474,6 +481,8 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     }
     if (tid == 0) {  // relaxed poll + one agent acquire (see lstm_resident_kernel)
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const bool tr = sync.handoff_trace && b == 0;
+      if (tr) g_lstm_handoff[0] = g_lstm_handoff[1] = t0;
       for (int r = ra; r <= rb; ++r)
         while (__hip_atomic_load(sync.ready + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
           __builtin_amdgcn_s_sleep(8);
@@ -484,6 +493,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
         }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tr) g_lstm_handoff[2] = __builtin_amdgcn_s_memrealtime();
     }
   }
   float c[4] = {0.f, 0.f, 0.f, 0.f};
@@ -625,8 +635,11 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (int cc = c0; cc < chunk; ++cc)
           __hip_atomic_fetch_add(sync.done + cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool tr = sync.handoff_trace && b == 0;
+        if (tr) g_lstm_handoff[3 + 3 * c0] = __builtin_amdgcn_s_memrealtime();
         if (chunk < sync.nr) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          if (tr) g_lstm_handoff[1 + 3 * chunk] = t0;
           while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
             __builtin_amdgcn_s_sleep(8);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
@@ -636,6 +649,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
           }
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (tr) g_lstm_handoff[2 + 3 * chunk] = __builtin_amdgcn_s_memrealtime();
         }
       }
       if (chunk < sync.nr) {  // rows t+1 and t+2 may have been prefetched before the hand-off: reload
@@ -782,6 +796,10 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
   sy.xplain = xplain;
   static const int xnowait = getenv("VAP_LSTM_XNOWAIT") ? atoi(getenv("VAP_LSTM_XNOWAIT")) : 0;  // timing diagnostics only
   sy.xnowait = xnowait;
+  static const int hot = getenv("VAP_LSTM_HANDOFF") ? atoi(getenv("VAP_LSTM_HANDOFF")) : 0;  // diagnostics
+  sy.handoff_trace = hot;
+  static const int wprio = getenv("VAP_LSTM_PRIO") ? atoi(getenv("VAP_LSTM_PRIO")) : 0;
+  sy.wave_prio = wprio;
   const int groups = (S + NS - 1) / NS;
   const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
   static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
@@ -812,6 +830,9 @@ template hipError_t launch_lstm<bf16>(const float*, int, int, const bf16*, bf16*
 template hipError_t launch_pack_whh<float>(const float*, float*, hipStream_t);
 template hipError_t launch_pack_whh<bf16>(const float*, bf16*, hipStream_t);
 
+hipError_t read_lstm_handoff(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_handoff), sizeof(g_lstm_handoff), 0, hipMemcpyDeviceToHost);
+}
 // diagnostics: copy the LSTM step stamps (8 workgroups x 4 steps x 5) to host memory
 hipError_t read_lstm_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_stamps), sizeof(g_lstm_stamps), 0, hipMemcpyDeviceToHost);

@@ -59,6 +59,8 @@ struct vap_handle {
   // "" = the even time_chunks split for both)
   // (the pair-split recurrence ends well before the caller stream's work: two back-end chunks, the
   // first of 640 frames = 5 full 128-query attention blocks, measured best: 156.2k -> 166.3k audio-s/s)
+  // (seven growing front-end pieces started the recurrence sooner in single-forward traces but
+  // measured 3.5 % slower in the back-to-back bench: kept as VAP_TC_FE=0.05,0.12,0.2,0.3,0.42,0.56,0.72)
   std::vector<double> tc_fe{0.1, 0.25, 0.45, 0.7}, tc_be{0.64};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
   bool heads_chunked = false;  // VAP_HEADS_CHUNKED=1: heads per back-end chunk (shorter tail after the
@@ -70,6 +72,16 @@ struct vap_handle {
   bool ffn_fused = true;  // bf16 FFN with the hidden in LDS (k_ffn.hip): 62 us vs 93 us for the unfused
                           // row-panel up + GEMM down per 32k rows; VAP_FFN_FUSED=0 selects the unfused pair
   hipStream_t side[NSIDE] = {};
+  // time-pipelined forward: conv2..4 + gate projections of each front-end piece on this high-priority
+  // stream while the caller stream runs the next piece's conv01, so each launch's last partial round
+  // of workgroups shares the chip with the other kernel (VAP_FE_STREAMS=1: all on the caller stream)
+  // (VAP_FE_STREAMS=2, session 4: within 1 % of one stream in the bench, +1.5 % in back-to-back
+  // forwards without per-launch timing events; one stream keeps each kernel's events clean)
+  hipStream_t fe_stream = nullptr;
+  int fe_streams = 1;
+  bool fe_first_serial = false;
+  int fe_gate = 0;  // VAP_FE_GATE: see conv_rows
+  bool fe_align = true;  // VAP_FE_ALIGN=0: conv1..3 ranges per piece exactly what its conv4 rows need
   hipEvent_t mb_ev[MAXMB] = {};
   hipEvent_t fork_ev[MAXMB] = {};
   int fork_next = 0;
@@ -106,8 +118,15 @@ struct vap_handle {
   const float* mono_hist = nullptr;
   int ensure_streams() {
     if (streams_ready) return VAP_OK;
-    for (auto& s : side)
-      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return VAP_ERR_HIP;
+    // side[1] doubles as the front-end stream of the time-pipelined forward (a stream of its own
+    // would share one of the process's GPU_MAX_HW_QUEUES hardware queues with another, which
+    // measured slower); VAP_FE_PRIO=1 creates it with the highest priority
+    static const int fe_prio = getenv("VAP_FE_PRIO") ? atoi(getenv("VAP_FE_PRIO")) : 1;
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) return VAP_ERR_HIP;
+    for (int i = 0; i < NSIDE; ++i)
+      if (hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, i == 1 && fe_prio ? prio_hi : prio_lo) != hipSuccess)
+        return VAP_ERR_HIP;
     for (int i = 0; i < MAXMB; ++i) {
       if (hipEventCreateWithFlags(&mb_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
       if (hipEventCreateWithFlags(&fork_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
@@ -144,6 +163,7 @@ struct vap_handle {
       if (err_host) (void)hipHostFree(err_host);
       if (xbuf) (void)hipFree(xbuf);
       for (auto& st : side) (void)hipStreamDestroy(st);
+      if (fe_stream && fe_stream != side[1]) (void)hipStreamDestroy(fe_stream);
       for (int i = 0; i < MAXMB; ++i) {
         (void)hipEventDestroy(mb_ev[i]);
         (void)hipEventDestroy(fork_ev[i]);
@@ -1308,8 +1328,12 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
 // bf16 CPC rows of conv4 range [a4, b4) of every sequence, with the conv1..conv3 rows they need
 // (k4 s2 p1 layers: rows [a, b) need input rows [2a-1, 2b+1) clipped to the layer; conv1 rows come
 // from the fused conv0->conv1 kernel straight from the waveform), then their LSTM gate projections.
+// With st2, conv2..4 and the gate projections run on st2 after an event on st (the caller keeps
+// st for the next piece's conv01).  done_lv (optional, in / out): rows [0, done_lv[i]) of conv(i+1)
+// exist already (an earlier piece of the same forward), so they are neither recomputed nor rewritten
+// while an earlier piece's conv2..4 may still read them.
 int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigned char* ws, bf16* GX, int64_t a4,
-              int64_t b4, hipStream_t st, int64_t gx_off = 0) {
+              int64_t b4, hipStream_t st, int64_t gx_off = 0, hipStream_t st2 = nullptr, int64_t* done_lv = nullptr) {
   using T = bf16;
   const int S = p.S;
   const int64_t* L = p.L;
@@ -1323,15 +1347,49 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     a[i] = std::max<int64_t>(0, 2 * a[i + 1] - 1);
     b[i] = std::min(L[i + 1], 2 * b[i + 1] + 1);
   }
-  {
+  if (done_lv) {
+    for (int i = 0; i < 3; ++i) a[i] = std::max(a[i], done_lv[i]);
+    // after the first piece, conv1..3 ranges are whole 256-row tiles from where the last piece
+    // stopped: the rows past what this piece needs are pulled forward from the next piece, not
+    // extra work, and only the first and the last piece launch a partial tile per sequence
+    for (int i = 2; i >= 0; --i) {
+      if (h->fe_align && a4 > 0) {
+        const int64_t need = std::min(L[i + 1], 2 * b[i + 1] + 1);
+        b[i] = std::min(L[i + 1], std::max(need, a[i] + (need - a[i] + 255) / 256 * 256));
+      }
+      b[i] = std::max(b[i], a[i]);
+    }
+  }
+  if (a[0] < b[0]) {
     Timed tm(h, VAP_K_CONV1, st);
     HIPCHK(launch_conv01(wav, S, N, (int)L[0], (int)L[1], (const bf16*)h->W<T>("conv0_op"), h->fpacked.at("conv0_stat"),
                          h->P(g + ".batchNorm0.bias"), (const bf16*)h->W<T>("conv1"), (const bf16*)h->W<T>("conv1_ks"), h->P(g + ".conv1.bias"),
                          h->P(g + ".batchNorm1.weight"), h->P(g + ".batchNorm1.bias"), (bf16*)(Xs[0] + D), p.s1, st,
                          (int)a[0], (int)b[0], device_cus() - (p.S + 15) / 16));  // the recurrence holds a CU per 16 sequences
   }
+  if (done_lv)
+    for (int i = 0; i < 3; ++i) done_lv[i] = b[i];
+  hipStream_t st0 = st;
+  if (st2) {
+    hipEvent_t fk = h->next_fork_event();
+    HIPCHK(hipEventRecord(fk, st));
+    HIPCHK(hipStreamWaitEvent(st2, fk, 0));
+    st = st2;
+  }
+  // VAP_FE_GATE=g (1..3): the caller stream's next launch (the next piece's conv01) waits until
+  // conv(g+1) of this piece is done, so it does not take the CUs those launches need first
+  auto gate = [&](int lvl) -> int {
+    if (st2 && h->fe_gate == lvl) {
+      hipEvent_t gk = h->next_fork_event();
+      HIPCHK(hipEventRecord(gk, st2));
+      HIPCHK(hipStreamWaitEvent(st0, gk, 0));
+    }
+    return VAP_OK;
+  };
   for (int i = 1; i < 4; ++i) {  // conv2..4 (encoder_components.py:100-103)
     const std::string cs = std::to_string(i + 1);
+    if (i > 1 && gate(i - 1)) return VAP_ERR_HIP;
+    if (a[i] >= b[i]) continue;
     Timed tm(h, VAP_K_CONV234, st);
     if (h->convk4) {
       ConvK4Args ca{Xs[i - 1] + a[i] * 2 * D, ss[i - 1], (int)(ss[i - 1] / D - 2 * a[i]), (const bf16*)h->W<T>("conv" + cs + "_ks"),
@@ -1348,6 +1406,7 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
     HIPCHK(gemm<T>(ga, st, false));
   }
+  if (gate(3)) return VAP_ERR_HIP;
   // gate projections of rows [a4, b4) into ring slots (r + gx_off) mod L4: at most two pieces
   Timed tm(h, VAP_K_LSTM_PROJ, st);
   for (int64_t r = a4; r < b4;) {
@@ -1376,15 +1435,30 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
   LstmSync sy;
   int rc;
   if ((rc = tc_launch_lstm(h, p, t, GX, ws, sy, st))) return rc;
-  int64_t done_rows = 0;
+  int64_t done_rows = 0, done_lv[3] = {0, 0, 0};
   int published = 0;
+  // conv2..4 + gate projections (and the ready flags) on the front-end stream, conv01 on st
+  // (timing mode, vap_timing: one stream, so each class's events bracket only its own kernels)
+  hipStream_t fst = h->fe_streams < 2 || h->timing_cls ? nullptr
+                    : h->fe_stream                   ? h->fe_stream
+                    : h->tc_streams < 2              ? h->side[1]
+                                                     : nullptr;
   for (int c = 0; c < t.nch; ++c) {  // front end, piece by piece (a piece ends at a front-end boundary)
     if (!t.fe_pub[c]) continue;
-    if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st))) return rc;
+    // VAP_FE_FIRST_SERIAL=1: the first piece all on st (its conv2..4 do not share the chip with the
+    // second piece's conv01, so the recurrence starts earlier)
+    const bool ser = h->fe_first_serial && done_rows == 0;
+    if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st, 0, ser ? nullptr : fst, done_lv))) return rc;
+
     done_rows = t.seq_end[c];
     for (; published <= c; ++published)
       if (published != h->test_drop_ready)
-        HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published), sy.epoch, 0));
+        HIPCHK(hipStreamWriteValue32(fst && !ser ? fst : st, (void*)(sy.ready + published), sy.epoch, 0));
+  }
+  if (fst) {  // join: the back end (and anything after the forward on st) follows the whole front end
+    hipEvent_t jn = h->next_fork_event();
+    HIPCHK(hipEventRecord(jn, fst));
+    HIPCHK(hipStreamWaitEvent(st, jn, 0));
   }
   return tc_back_end(h, p, t, sy, ws, logits, vadl, st);
 }
@@ -1808,6 +1882,10 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);
+  if (const char* e = getenv("VAP_FE_STREAMS")) h->fe_streams = atoi(e);
+  if (const char* e = getenv("VAP_FE_ALIGN")) h->fe_align = atoi(e) != 0;
+  if (const char* e = getenv("VAP_FE_FIRST_SERIAL")) h->fe_first_serial = atoi(e) != 0;
+  if (const char* e = getenv("VAP_FE_GATE")) h->fe_gate = atoi(e);
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);

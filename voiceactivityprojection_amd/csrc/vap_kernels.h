@@ -112,7 +112,12 @@ struct LstmSync {
   unsigned xepoch = 0;  // lstm_pair: launch epoch in the exchange tags (set by launch_lstm_pair)
   int xplain = 0;       // lstm_pair: exchange stores with the default policy (experiment)
   int xnowait = 0;      // lstm_pair: do not wait for the partner (timing diagnostics; outputs are garbage)
+  int wave_prio = 0;  // lstm_pair (VAP_LSTM_PRIO): waves 0-3 at this s_setprio level, 4-7 at 0 (experiment)
+  int handoff_trace = 0;  // lstm_pair (VAP_LSTM_HANDOFF=1): workgroup 0 records s_memrealtime around each hand-off
 };
+// diagnostics: [0] launch start, then per time chunk c: [1 + 3c] ready wait begins, [2 + 3c] ready seen,
+// [3 + 3c] done published (s_memrealtime, 100 MHz) of the last lstm_pair launch with handoff_trace
+hipError_t read_lstm_handoff(unsigned long long* out);
 // prescaled: W_ih / W_hh / biases packed with the gate scales (launch_pack_wih_prescaled,
 // launch_pack_whh_resident(.., true)): gates arrive as -log2e (i, f, o) / 2 log2e (g) multiples
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,
