@@ -21,6 +21,8 @@
 //   * epilogue: the accumulators start at the bias; ChannelNorm from ONE exchange of per-wave
 //     (mean, M2) pairs over its 32 channels (Chan's parallel variance), gamma / beta from LDS, ReLU,
 //     16-B bf16 stores assembled with v_permlane32_swap.
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "vap_common.h"
@@ -36,10 +38,27 @@ constexpr int CK_HALF = CK_HR * 64;        // 17408 B
 constexpr int CK_SLAB = 2 * CK_HALF;       // 34816 B
 constexpr int CK_RED = 3 * CK_SLAB;        // 104448: [256 rows][8 waves] (mean, M2) float2 (epilogue)
 constexpr int CK_PAR = CK_RED + 256 * 8 * 8;  // 120832: bias | gamma | beta, 3 x 256 fp32
-constexpr int CK_LDS = CK_PAR + 3 * 256 * 4;  // 123904 B
+constexpr int CK_ST = CK_PAR + 3 * 256 * 4;   // 123904: 12 phase stamps (VAP_CONVK4_DBG=16)
+constexpr int CK_LDS = CK_ST + 12 * 8;        // 124000 B
 constexpr int CK_PIECES = 2 * (CK_HR / 16);  // 34 DMA pieces of 16 half-rows x 64 B per slab
 
 VAP_DEV int ck_phys(int row, int c) { return (c + (row >> 2)) & 3; }
+// x + x of lane ^ 32: v_permlane32_swap of two copies leaves the low half's values in one and the
+// high half's in the other, in every lane (no lane id, no LDS permute)
+// (inline asm: given equal operands, hipcc took the builtin's two results for one value and added
+// a result to itself)
+VAP_DEV float ck_xsum(float x) {
+  float a = x, b = x;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  return a + b;
+}
+// the lane id rebuilt by volatile asm at each use: per-lane constants derived from it cannot be
+// hoisted out of the persistent tile loop (there they held registers and were spilled to scratch)
+VAP_DEV int ck_lane() {
+  int ln;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  return ln;
+}
 VAP_DEV void ck_mfma(f32x16& c, const chunk16& a, const chunk16& b) {
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
@@ -53,19 +72,23 @@ VAP_DEV uint32_t ck_relu2(float a, float b) {  // bf16(max(x, 0)) for two values
 }
 
 template <int DBG>
-__global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
+__global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, int ntiles) {
+  // Persistent: workgroup b runs tiles b, b + G, b + 2G, ... (G = gridDim.x <= the CUs free beside
+  // the recurrence).  Tile (s, tb) = output rows 256 tb .. of sequence s.  The next tile's first two
+  // slabs and W fragments are issued during the current tile's last two blocks, so its loads land
+  // while this tile's epilogue runs (one-tile-per-launch spent ~7k of ~68k cycles per tile waiting
+  // for them).  The global block counter gidx = 8 * (tiles done) + CB picks the slab slot gidx % 3.
   __shared__ __attribute__((aligned(16))) unsigned char smem[CK_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32w .. 32w+31
-  const int s = blockIdx.y;
-  const int t0 = blockIdx.x * 256;
-  const bf16* in = a.in + (int64_t)s * a.in_seq_stride;
-  unsigned long long stv[12];
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
   int nst = 0;
-  auto stamp = [&]() {
+  auto stamp = [&]() {  // (to LDS: held in registers across the tile loop they were spilled)
     if constexpr ((DBG & 16) != 0) {
       __builtin_amdgcn_sched_barrier(0);
-      if (nst < 12) stv[nst] = __builtin_amdgcn_s_memtime();
+      const unsigned long long v = __builtin_amdgcn_s_memtime();
+      if (nst < 12 && tid == 0) ((unsigned long long*)(smem + CK_ST))[nst] = v;
       ++nst;
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -78,209 +101,290 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a) {
 
   // ---- DMA of input block cb (channels 32cb..) into slot sl: pieces q = w + 8k (34 per slab)
   // Every wave issues 5 pieces (waves 2..7 repeat their 4th: the same bytes to the same place), so
-  // the DMA count per wave is uniform and the compiler can count vmcnt past it (a branch around the
-  // 5th piece made it fall back to vmcnt(0) before each block's first MFMA).
+  // the DMA count per wave is uniform and the hand-counted vmcnt waits hold for every wave.
   auto piece = [&](int k) { return k == 4 && w >= 2 ? w + 24 : w + 8 * k; };
-  uint32_t dsrc[5];               // element offsets (channel block 0) of this lane's source per piece
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int q = piece(k);
+  // per piece k: the lane's source row within the tile's slab (2 hr + hb) << 8 | its chunk offset
+  // (logical chunk held at physical chunk lane%4) x 8 elements; tile rows start at input row 2 t0.
+  // Recomputed from an opaque copy of the lane id at each use: hoisted out of the tile loop, these
+  // per-lane constants spilled to scratch (and every reload waited for all loads in flight).
+  auto prow = [&](int k) -> uint32_t {
+    const int ln = ck_lane();
+    int wo = w;
+    asm volatile("" : "+s"(wo));
+    const int q = k == 4 && wo >= 2 ? wo + 24 : wo + 8 * k;
     const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
-    const int hr = 16 * p + (lane >> 2);
-    const int c = ((lane & 3) - (hr >> 2)) & 3;  // logical chunk held at physical chunk lane%4
-    const int row = min(2 * t0 + 2 * hr + hb, a.in_rows - 1);  // rows past the range feed no stored output
-    dsrc[k] = (uint32_t)(row * 256 + c * 8);
-  }
+    const int hr = 16 * p + (ln >> 2);
+    const int c = ((ln & 3) - (hr >> 2)) & 3;
+    return (uint32_t)(((2 * hr + hb) << 8) | (c * 8));
+  };
+  struct TileSrc {
+    const bf16* in;  // sequence base
+    int t0;          // first output row
+  };
+  auto tile_src = [&](int tl, int& s_) {
+    s_ = tl / ntb;
+    return TileSrc{a.in + (int64_t)s_ * a.in_seq_stride, (tl - s_ * ntb) * 256};
+  };
   // Both the slab DMA and the W loads are inline asm with hand-counted waits: the compiler treats a
   // global_load_lds as an LDS write that may alias every later ds_read and put vmcnt(0) before each
   // block's first MFMA, draining the two-block-deep DMA stream.  Per block the wave issues, in order,
   // W(CB+1) (8 loads) then DMA(CB+2) (5 pieces); at the start of block CB, vmcnt(5) leaves only
   // DMA(CB+1) in flight, so W(CB) and DMA(CB) have landed.
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  auto dma = [&](int cb, int sl) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
+  auto dma1 = [&](const TileSrc& ts, int cb, int sl, int k) {
+    {
       const int q = piece(k);
       const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
-      const bf16* src = in + dsrc[k] + cb * 32;
+      const uint32_t pr = prow(k);
+      const int row = min(2 * ts.t0 + (int)(pr >> 8), a.in_rows - 1);  // rows past the range feed no stored output
+      const bf16* src = ts.in + (row * 256 + (int)(pr & 255u) + cb * 32);
       const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(sl * CK_SLAB + hb * CK_HALF + p * 1024));
       uint32_t keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
     }
   };
+  auto dma = [&](const TileSrc& ts, int cb, int sl) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dma1(ts, cb, sl, k);
+  };
   // ---- W fragments of block cb: [tap j][k half kh] (A of the 32x32x16: channel 32w + lane%32)
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.W, 32 * 256 * 64);
-  const uint32_t wlo = (uint32_t)((w * 32 + (lane & 31)) * 64 + (lane >> 5) * 16);
-  auto wload = [&](int cb, chunk16* wf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(wf[j * 2 + kh])
-                     : "v"(wlo), "s"(wrs), "s"((j * 8 + cb) * 16384 + kh * 32) : "memory");
+  // fragment f = 2j + kh of block cb (tap j, k half kh).  The lane offset is rebuilt once per block
+  // (kept live through the tile loop it was spilled) and passed in: computed next to the refill, its
+  // VALU writes landed in the registers of the fragment the MFMA just issued was still reading.
+  auto wlane = [&]() -> uint32_t {
+    const int ln = ck_lane();
+    return (uint32_t)((w * 32 + (ln & 31)) * 64 + (ln >> 5) * 16);
+  };
+  auto wload1 = [&](uint32_t wlo, int cb, int f, chunk16& wf) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(wf)
+                 : "v"(wlo), "s"(wrs), "s"(((f >> 1) * 8 + cb) * 16384 + (f & 1) * 32) : "memory");
   };
 
   // the accumulators start at the bias (lane element e: channel 32w + 8(e/4) + 4(lane/32) + e%4)
   const int cb0 = w * 32 + 4 * (lane >> 5);
+  const float* PR = (const float*)(smem + CK_PAR);
+  __syncthreads();  // parameters in LDS
   f32x16 acc[8];
-  {
-    const float* PR = (const float*)(smem + CK_PAR);
-    __syncthreads();  // parameters in LDS
+  auto acc_init = [&]() {
     f32x4 bb[4];
+    const int c0 = w * 32 + 4 * (ck_lane() >> 5);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(PR + cb0 + 8 * q);
+    for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(PR + c0 + 8 * q);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][e] = bb[e >> 2][e & 3];
-  }
-  // write the accumulators HERE, with the wait states an MFMA reading them as SrcC needs after the
-  // v_accvgpr writes (the MFMAs are inline asm, invisible to the compiler's hazard recognizer;
-  // left alone it sank each tile's zeroing to just before its first MFMA)
-  asm volatile("s_nop 4" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
-  asm volatile("s_nop 4" : "+a"(acc[4]), "+a"(acc[5]), "+a"(acc[6]), "+a"(acc[7]));
+    // write the accumulators HERE, with the wait states an MFMA reading them as SrcC needs after the
+    // v_accvgpr writes (the MFMAs are inline asm, invisible to the compiler's hazard recognizer;
+    // left alone it sank each tile's zeroing to just before its first MFMA)
+    asm volatile("s_nop 4" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+    asm volatile("s_nop 4" : "+a"(acc[4]), "+a"(acc[5]), "+a"(acc[6]), "+a"(acc[7]));
+  };
 
+  int s;
+  TileSrc cur = tile_src(tile, s);
+  // Two sets of W fragments (block CB in set CB % 2).  Issue order per wave and block CB: W(CB+1)
+  // (8 loads) then DMA(CB+2) (5 pieces) at the block start, so at the start of block CB, vmcnt(5)
+  // leaves only DMA(CB+1) in flight: W(CB) and DMA(CB) have landed.  Across tiles: blocks 6 / 7 issue
+  // the next tile's DMA(0) / DMA(1); its W(0) goes out after the epilogue's stores (live through the
+  // epilogue, the fragments were spilled to scratch right after their loads were issued), so its
+  // block 0 waits with vmcnt(0).  (One W set refilled fragment by fragment measured slower: a refill
+  // issued after DMA(CB+1) made each fragment wait for that slab too.)
   chunk16 W[2][8];
-  wload(0, W[0]);
-  dma(0, 0);
-  dma(1, 1);
+  {
+    const uint32_t wlo = wlane();
+#pragma unroll
+    for (int f = 0; f < 8; ++f) wload1(wlo, 0, f, W[0][f]);
+  }
+  dma(cur, 0, 0);
+  dma(cur, 1, 1);
 
   // G fragment (tap j, k half kh, row tile i) -> half j%2, rows 32i + lane%32 + j/2.  The swizzle
   // depends on the lane, j/2 and kh only (32i is a multiple of 4 rows), so a block reads through four
   // lane bases (+ the slot, set per block) and immediate offsets (half, row tile)
-  uint32_t gbase0[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
+  auto gbase0 = [&](int v) -> uint32_t {
+    const int ln = ck_lane();
     const int jh = v >> 1, kh = v & 1;
-    const int row = (lane & 31) + jh;
-    gbase0[v] = (uint32_t)(row * 64 + ck_phys(row, 2 * kh + (lane >> 5)) * 16);
-  }
-  auto block = [&](auto cbc, chunk16* wf, chunk16* wn) {
-    constexpr int CB = decltype(cbc)::value, SL = CB % 3;
-    uint32_t gb[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      gb[v] = gbase0[v] + SL * CK_SLAB;
-      asm volatile("" : "+v"(gb[v]));  // materialised here, not hoisted out of the blocks
-    }
-    auto gread = [&](int sl, int j, int kh, int i) -> chunk16 {
-      (void)sl;
-      return *(const chunk16*)(smem + gb[(j >> 1) * 2 + kh] + (j & 1) * CK_HALF + i * 2048);
-    };
-    // own DMA of block CB and W of CB landed (younger: only block CB+1's DMA pieces)
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (CB + 1 < 8) {
-      asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of CB landed; slot (CB+2)%3 fully read
-    __builtin_amdgcn_sched_barrier(0);
-    stamp();
-    if constexpr (CB + 1 < 8) wload(CB + 1, wn);
-    if constexpr (CB + 2 < 8) dma(CB + 2, (CB + 2) % 3);
-    constexpr int GA = 3;
-    chunk16 gf[GA + 1];
-#pragma unroll
-    for (int n = 0; n < GA; ++n) gf[n] = gread(SL, n >> 4, (n >> 3) & 1, n & 7);
-#pragma unroll
-    for (int n = 0; n < 64; ++n) {  // n = 16j + 8kh + i
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((DBG & 6) != 0) {
-        const chunk16 one = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-        ck_mfma(acc[n & 7], (DBG & 4) ? one : wf[n >> 3], (DBG & 2) ? one : gf[n & GA]);
-      } else {
-        ck_mfma(acc[n & 7], wf[n >> 3], gf[n & GA]);
-      }
-      const int m = n + GA;
-      if (m < 64) gf[m & GA] = gread(SL, m >> 4, (m >> 3) & 1, m & 7);
-    }
+    const int row = (ln & 31) + jh;
+    return (uint32_t)(row * 64 + ck_phys(row, 2 * kh + (ln >> 5)) * 16);
   };
-  block(std::integral_constant<int, 0>{}, W[0], W[1]);
-  block(std::integral_constant<int, 1>{}, W[1], W[0]);
-  block(std::integral_constant<int, 2>{}, W[0], W[1]);
-  block(std::integral_constant<int, 3>{}, W[1], W[0]);
-  block(std::integral_constant<int, 4>{}, W[0], W[1]);
-  block(std::integral_constant<int, 5>{}, W[1], W[0]);
-  block(std::integral_constant<int, 6>{}, W[0], W[1]);
-  block(std::integral_constant<int, 7>{}, W[1], W[0]);
-
-  stamp();
-  // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[row = i*32 + lane%32][channel 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15 (+ bias)
-#pragma unroll
-  for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
-                 : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
-  const float* PR = (const float*)(smem + CK_PAR);
   float2* red = (float2*)(smem + CK_RED);  // [256 rows][8 waves] (mean, M2) of the wave's 32 channels
-  auto val = [&](int i, int q) -> f32x4 {
-    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
-  };
+  int gs = 0;          // (8 x tiles done) % 3: slot of this tile's block 0
+  bool first = true;
+  for (;;) {
+    const int nxt = tile + (int)gridDim.x;
+    const bool has_next = nxt < ntiles;
+    int sn = 0;
+    const TileSrc nx = tile_src(has_next ? nxt : tile, sn);
+    const int t0 = cur.t0;
+    acc_init();
+    auto block = [&](auto cbc) {
+      constexpr int CB = decltype(cbc)::value;
+      chunk16* wf = W[CB & 1];
+      chunk16* wn = W[(CB + 1) & 1];
+      int sl = gs + CB;
+      sl = sl >= 6 ? sl - 6 : sl >= 3 ? sl - 3 : sl;
+      int sl2 = sl + 2;
+      sl2 = sl2 >= 3 ? sl2 - 3 : sl2;
+      uint32_t gb[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
-    float sum = (t[0] + t[1]) + (t[2] + t[3]);
-    sum += __shfl_xor(sum, 32, 64);
-    const float mw = sum * (1.0f / 32);
-    f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 d = val(i, q) - mw;
-      d2 += d * d;
-    }
-    float m2 = (d2[0] + d2[1]) + (d2[2] + d2[3]);
-    m2 += __shfl_xor(m2, 32, 64);
-    if (lane < 32) red[(i * 32 + lane) * 8 + w] = float2{mw, m2};
-  }
-  __syncthreads();
-  bf16* obase = a.out + (int64_t)s * a.out_seq_stride;
-  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)a.M * 256 * 2));
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    // Chan: 8 groups of 32 channels: mean = mean of the group means, M2 = sum M2_w + 32 sum (m_w - m)^2
-    const f32x4* rp = (const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
-    const f32x4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-    const float m = (((r0[0] + r0[2]) + (r1[0] + r1[2])) + ((r2[0] + r2[2]) + (r3[0] + r3[2]))) * 0.125f;
-    auto dev = [&](float mw) { return (mw - m) * (mw - m); };
-    const float M2 = (((r0[1] + r0[3]) + (r1[1] + r1[3])) + ((r2[1] + r2[3]) + (r3[1] + r3[3]))) +
-                     32.0f * (((dev(r0[0]) + dev(r0[2])) + (dev(r1[0]) + dev(r1[2]))) +
-                              ((dev(r2[0]) + dev(r2[2])) + (dev(r3[0]) + dev(r3[2]))));
-    const float rstd = rsqrtf(M2 * (1.0f / 255) + 1e-5f);
-    const int t = t0 + i * 32 + (lane & 31);
-    uint32_t pk[4][2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 gg = *(const f32x4*)(PR + 256 + cb0 + 8 * q), ee = *(const f32x4*)(PR + 512 + cb0 + 8 * q);
-      const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - m) * rstd * gg + ee;
-      if constexpr ((DBG & 1) != 0) {
-        pk[q][0] = pack_bf16x4(v[0], v[1], v[2], v[3])[0];
-        pk[q][1] = pack_bf16x4(v[0], v[1], v[2], v[3])[1];
+      for (int v = 0; v < 4; ++v) {
+        gb[v] = gbase0(v) + sl * CK_SLAB;
+        asm volatile("" : "+v"(gb[v]));  // materialised here, not hoisted out of the blocks
+      }
+      auto gread = [&](int j, int kh, int i) -> chunk16 {
+        return *(const chunk16*)(smem + gb[(j >> 1) * 2 + kh] + (j & 1) * CK_HALF + i * 2048);
+      };
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (CB == 0) {
+        if (first) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else if constexpr (CB < 7) {
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
       } else {
-        pk[q][0] = ck_relu2(v[0], v[1]);
-        pk[q][1] = ck_relu2(v[2], v[3]);
+        if (has_next) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_barrier" ::: "memory");  // every wave's pieces of CB landed; slot (CB+2)%3 fully read
+      __builtin_amdgcn_sched_barrier(0);
+      stamp();
+      if constexpr (CB + 1 < 8) {
+        const uint32_t wlo = wlane();
+#pragma unroll
+        for (int f = 0; f < 8; ++f) wload1(wlo, CB + 1, f, wn[f]);
+      }
+      // DMA(CB+2): one piece every 8 MFMAs (n = 4, 12, .., 36), its address math in the MFMA stream
+      // (issued together after the barrier it cost ~1-2k cycles per block before the first MFMA)
+      constexpr int GA = 3;
+      chunk16 gf[GA + 1];
+#pragma unroll
+      for (int n = 0; n < GA; ++n) gf[n] = gread(n >> 4, (n >> 3) & 1, n & 7);
+#pragma unroll
+      for (int n = 0; n < 64; ++n) {  // n = 16j + 8kh + i
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((DBG & 6) != 0) {
+          const chunk16 one = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+          ck_mfma(acc[n & 7], (DBG & 4) ? one : wf[n >> 3], (DBG & 2) ? one : gf[n & GA]);
+        } else {
+          ck_mfma(acc[n & 7], wf[n >> 3], gf[n & GA]);
+        }
+        const int m = n + GA;
+        if (m < 64) gf[m & GA] = gread(m >> 4, (m >> 3) & 1, m & 7);
+        if ((n & 7) == 4 && n < 40) {
+          if constexpr (CB + 2 < 8) dma1(cur, CB + 2, sl2, n >> 3);
+          else if (has_next) dma1(nx, CB - 6, sl2, n >> 3);
+        }
+      }
+    };
+    block(std::integral_constant<int, 0>{});
+    block(std::integral_constant<int, 1>{});
+    block(std::integral_constant<int, 2>{});
+    block(std::integral_constant<int, 3>{});
+    block(std::integral_constant<int, 4>{});
+    block(std::integral_constant<int, 5>{});
+    block(std::integral_constant<int, 6>{});
+    block(std::integral_constant<int, 7>{});
+
+    stamp();
+    // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+    // lane holds C[row = i*32 + lane%32][channel 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15 (+ bias)
+#pragma unroll
+    for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                   : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
+    auto val = [&](int i, int q) -> f32x4 {
+      return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);  // row tiles one after another (interleaved, they spilled)
+      const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
+      float sum = (t[0] + t[1]) + (t[2] + t[3]);
+      sum = ck_xsum(sum);
+      const float mw = sum * (1.0f / 32);
+      f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 d = val(i, q) - mw;
+        d2 += d * d;
+      }
+      float m2 = (d2[0] + d2[1]) + (d2[2] + d2[3]);
+      m2 = ck_xsum(m2);
+      const int ln = ck_lane();
+      if (ln < 32) red[(i * 32 + ln) * 8 + w] = float2{mw, m2};
+    }
+    // LDS only (a __syncthreads would also wait for the next tile's slab DMA in flight); the barrier
+    // as asm with a memory clobber: the s_barrier builtin does not order memory, and the compiler
+    // hoisted the reads of `red` above it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    bf16* obase = a.out + (int64_t)s * a.out_seq_stride;
+    const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)a.M * 256 * 2));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      // Chan: 8 groups of 32 channels: mean = mean of the group means, M2 = sum M2_w + 32 sum (m_w - m)^2
+      const int ln = ck_lane();
+      const f32x4* rp = (const f32x4*)(red + (i * 32 + (ln & 31)) * 8);
+      const f32x4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+      const float m = (((r0[0] + r0[2]) + (r1[0] + r1[2])) + ((r2[0] + r2[2]) + (r3[0] + r3[2]))) * 0.125f;
+      auto dev = [&](float mw) { return (mw - m) * (mw - m); };
+      const float M2 = (((r0[1] + r0[3]) + (r1[1] + r1[3])) + ((r2[1] + r2[3]) + (r3[1] + r3[3]))) +
+                       32.0f * (((dev(r0[0]) + dev(r0[2])) + (dev(r1[0]) + dev(r1[2]))) +
+                                ((dev(r2[0]) + dev(r2[2])) + (dev(r3[0]) + dev(r3[2]))));
+      const float rstd = rsqrtf(M2 * (1.0f / 255) + 1e-5f);
+      const int t = t0 + i * 32 + (ln & 31);
+      uint32_t pk[4][2];
+      // gamma / beta re-read from LDS per row tile (hoisted out of the loop they would hold 32 VGPRs
+      // through the epilogue, beside the next tile's W fragments already in flight)
+      const uint32_t pro = (uint32_t)((w * 32 + 4 * (ln >> 5)) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 gg = *(const f32x4*)((const unsigned char*)PR + 1024 + pro + 32 * q);
+        const f32x4 ee = *(const f32x4*)((const unsigned char*)PR + 2048 + pro + 32 * q);
+        const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - m) * rstd * gg + ee;
+        if constexpr ((DBG & 1) != 0) {
+          pk[q][0] = pack_bf16x4(v[0], v[1], v[2], v[3])[0];
+          pk[q][1] = pack_bf16x4(v[0], v[1], v[2], v[3])[1];
+        } else {
+          pk[q][0] = ck_relu2(v[0], v[1]);
+          pk[q][1] = ck_relu2(v[2], v[3]);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+          pk[2 * p][d] = sw[0];
+          pk[2 * p + 1][d] = sw[1];
+        }
+        const int col = w * 32 + 8 * (2 * p + (ln >> 5));
+        const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+        buf_store16(orsc, t < a.M ? (uint32_t)((t * 256 + col) * 2) : 0xFFFFFFF0u, o);
       }
     }
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
-        pk[2 * p][d] = sw[0];
-        pk[2 * p + 1][d] = sw[1];
+    if constexpr ((DBG & 16) != 0) {
+      if (first) {
+        stamp();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp();
+        if (s == 0 && t0 < 8 * 256 && tid == 0)
+          for (int k = 0; k < 12; ++k) a.stamps[(t0 >> 8) * 12 + k] = ((const unsigned long long*)(smem + CK_ST))[k];
       }
-      const int col = w * 32 + 8 * (2 * p + (lane >> 5));
-      const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
-      buf_store16(orsc, t < a.M ? (uint32_t)((t * 256 + col) * 2) : 0xFFFFFFF0u, o);
     }
-  }
-  if constexpr ((DBG & 16) != 0) {
-    stamp();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
-    if (s == 0 && blockIdx.x < 8 && tid == 0)
-      for (int k = 0; k < 12; ++k) a.stamps[blockIdx.x * 12 + k] = stv[k];
+    if (!has_next) break;
+    {  // the next tile's W(0), after this tile's stores
+      const uint32_t wlo = wlane();
+#pragma unroll
+      for (int f = 0; f < 8; ++f) wload1(wlo, 0, f, W[0][f]);
+    }
+    first = false;
+    tile = nxt;
+    s = sn;
+    cur = nx;
+    gs = gs + 2 >= 3 ? gs - 1 : gs + 2;  // (gs + 8) % 3
   }
 }
 
@@ -291,13 +395,22 @@ hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
   if (a.in_seq_stride % 8 || a.out_seq_stride % 8)
     return hipErrorInvalidValue;
   if ((int64_t)a.M * 256 * 2 >= (1ll << 32) || (int64_t)a.in_rows * 256 >= (1ll << 31)) return hipErrorInvalidValue;
-  const dim3 grid((a.M + 255) / 256, S);
+  const int ntb = (a.M + 255) / 256, ntiles = ntb * S;
+  // persistent: at most one workgroup per CU free beside the recurrence (a.grid_cap, 0 = all CUs);
+  // one tile per workgroup when the tiles fit in one round anyway
+  // Default: one tile per workgroup.  The persistent form (VAP_CONVK4_PERSIST=1, workgroups capped at
+  // a.grid_cap) measured slower in the bench (conv2..4 1.75 vs 1.50 ms per step): its next tile's
+  // block 0 waits for the epilogue stores and W(0), and static striding balances worse than the
+  // dispatcher handing tiles to whichever CU frees up.
+  static const bool persist = getenv("VAP_CONVK4_PERSIST") != nullptr;
+  const int cap = persist ? (a.grid_cap > 0 ? a.grid_cap : 256) : ntiles;
+  const dim3 grid(std::min(ntiles, cap));
   switch (a.dbg) {
-    case 0: hipLaunchKernelGGL(convk4_kernel<0>, grid, dim3(512), 0, st, a); break;
-    case 1: hipLaunchKernelGGL(convk4_kernel<1>, grid, dim3(512), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(convk4_kernel<3>, grid, dim3(512), 0, st, a); break;
-    case 5: hipLaunchKernelGGL(convk4_kernel<5>, grid, dim3(512), 0, st, a); break;
-    case 16: hipLaunchKernelGGL(convk4_kernel<16>, grid, dim3(512), 0, st, a); break;
+    case 0: hipLaunchKernelGGL(convk4_kernel<0>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
+    case 1: hipLaunchKernelGGL(convk4_kernel<1>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
+    case 3: hipLaunchKernelGGL(convk4_kernel<3>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
+    case 5: hipLaunchKernelGGL(convk4_kernel<5>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
+    case 16: hipLaunchKernelGGL(convk4_kernel<16>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

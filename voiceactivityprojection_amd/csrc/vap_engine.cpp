@@ -189,6 +189,8 @@ struct vap_handle {
 
 namespace {
 
+static int conv_grid_cap(const vap_handle* h, int S);
+
 void add_schema(vap_handle* h) {
   auto add = [&](const std::string& k, int64_t n) {
     h->keys.push_back(k);
@@ -793,6 +795,7 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
         ConvK4Args ca{(const bf16*)ins[i], in_ss[i], (int)(in_ss[i] / D), (const bf16*)h->W<T>("conv" + c + "_ks"),
                       h->P(g + ".conv" + c + ".bias"), h->P(g + ".batchNorm" + c + ".weight"),
                       h->P(g + ".batchNorm" + c + ".bias"), (bf16*)(Xs[i] + D), ss[i], (int)L[i + 1]};
+        ca.grid_cap = conv_grid_cap(h, S);
         HIPCHK(launch_convk4(ca, S, st));
         continue;
       }
@@ -1067,6 +1070,10 @@ static int rec_workgroups(const vap_handle* h, int S) { return h->lstm_pair ? ls
 // groups of 16 sequences one persistent launch may take (at least one, whatever the cap)
 static int rec_group_cap(const vap_handle* h) { return std::max(1, lstm_wg_cap(h) / (h->lstm_pair ? 2 : 1)); }
 static bool persistent_fits(const vap_handle* h, int S) { return (S + 15) / 16 <= rec_group_cap(h); }
+// workgroups of a persistent conv launch: the CUs the recurrence running beside it leaves free
+static int conv_grid_cap(const vap_handle* h, int S) {
+  return device_cus() - std::min(rec_workgroups(h, S), lstm_wg_cap(h));
+}
 
 // The bf16 recurrence of S sequences (gate rows GX [S][L4][1024], h rows to out): the pair split
 // (default) or the single-CU resident kernel.  xg0 offsets the launch's slots in the exchange buffer
@@ -1395,6 +1402,7 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
       ConvK4Args ca{Xs[i - 1] + a[i] * 2 * D, ss[i - 1], (int)(ss[i - 1] / D - 2 * a[i]), (const bf16*)h->W<T>("conv" + cs + "_ks"),
                     h->P(g + ".conv" + cs + ".bias"), h->P(g + ".batchNorm" + cs + ".weight"),
                     h->P(g + ".batchNorm" + cs + ".bias"), Xs[i] + D + a[i] * D, ss[i], (int)(b[i] - a[i])};
+      ca.grid_cap = conv_grid_cap(h, S);
       HIPCHK(launch_convk4(ca, S, st));
       continue;
     }

@@ -43,6 +43,7 @@ struct ConvK4Args {
   int dbg = 0;  // diagnostics (tools/diag_convk4.py): 1 raw conv + bias out, 2 G := 1, 4 W := 1,
                 // 16 phase stamps of workgroups (0..7, seq 0) into stamps[8][12]
   unsigned long long* stamps = nullptr;
+  int grid_cap = 0;  // workgroups of the persistent launch (the CUs free beside the recurrence; 0: all)
 };
 hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st);
 // bf16 256x256-tile LDS-DMA variant (k_gemm2.hip); launch_gemm<bf16, *> dispatches to it
