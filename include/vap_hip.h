@@ -152,6 +152,12 @@ int vap_probs(const float* logits, const float* vad_logits, int batch, int frame
  * entropy loss [B][T - horizon] of logits [B][T][256] against them (logits and loss may both be
  * NULL: labels only).  bin_frames is a HOST array of n_bins frame counts (bin_times_to_frames,
  * vap/objective.py:10-11). */
+/* VapGPT.probs epilogue in one call (vap/model.py:180-225): vap_probs' outputs plus labels [B][T-h] and
+ * loss [B][T-h] of vap_labels_loss, with the labels taken from sigmoid(vad_logits) (quirk Q1); h = the
+ * sum of bin_frames (at most 128).  Same values as vap_probs followed by vap_labels_loss on its vad. */
+int vap_probs_loss(const float* logits, const float* vad_logits, int batch, int frames, int n_bins, int now0, int now1,
+                   int fut0, int fut1, const int* bin_frames, float threshold, float* probs, float* vad, float* p_now,
+                   float* p_future, float* H, int64_t* labels, float* loss, void* stream);
 int vap_labels_loss(const float* logits, const float* va, int batch, int frames, const int* bin_frames, int n_bins,
                     float threshold, int64_t* labels, float* loss, void* stream);
 

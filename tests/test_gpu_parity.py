@@ -273,3 +273,38 @@ def test_attention_maps_bf16_vs_oracle(m16):
         assert got.shape == exp.shape, (k, got.shape, exp.shape)
         err = float(np.abs(got - exp).max())
         assert err < 3e-2, f"{k}: {err}"
+
+
+@pytest.mark.parametrize("B,T", [(3, 130), (2, 1000), (1, 101)])
+def test_probs_loss_fused_equals_two_calls(m32, B, T):
+    """vap_probs_loss (VapGPT.probs' epilogue: labels through LDS from the VAD logits, loss inside the
+    softmax pass) is bit-identical to vap_probs followed by vap_labels_loss on vap_probs' vad."""
+    import ctypes
+
+    from voiceactivityprojection_amd import _native as N
+
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    logits = (torch.randn(B, T, 256, generator=g) * 3).cuda()
+    vadl = (torch.randn(B, T, 2, generator=g) * 2).cuda()
+    obj = m32.objective
+    n = T - obj.horizon
+    bf = (ctypes.c_int * 4)(*obj.bin_frames)
+    st = N.stream_ptr(logits.device)
+    outs = []
+    for fused in (False, True):
+        o = {k: torch.empty(B, T, 256 if k == "probs" else 2, device="cuda") for k in ("probs", "vad", "p_now", "p_future")}
+        o["H"] = torch.empty(B, T, device="cuda")
+        o["labels"] = torch.empty(B, n, dtype=torch.int64, device="cuda")
+        o["loss"] = torch.empty(B, n, device="cuda")
+        ptrs = [o[k].data_ptr() for k in ("probs", "vad", "p_now", "p_future", "H")]
+        if fused:
+            N.check(N.lib().vap_probs_loss(logits.data_ptr(), vadl.data_ptr(), B, T, 4, 0, 1, 2, 3, bf, 0.5, *ptrs,
+                                           o["labels"].data_ptr(), o["loss"].data_ptr(), st), "vap_probs_loss")
+        else:
+            N.check(N.lib().vap_probs(logits.data_ptr(), vadl.data_ptr(), B, T, 4, 0, 1, 2, 3, *ptrs, st), "vap_probs")
+            N.check(N.lib().vap_labels_loss(logits.data_ptr(), o["vad"].data_ptr(), B, T, bf, 4, 0.5,
+                                            o["labels"].data_ptr(), o["loss"].data_ptr(), st), "vap_labels_loss")
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu() for k, v in o.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k

@@ -56,6 +56,8 @@ _SIGS = {
     "vap_probs": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "vap_aggregate": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]),
+    "vap_probs_loss": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vap_labels_loss": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.c_float, _P, _P,
                                        _P]),
     "vap_vad_postprocess": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,

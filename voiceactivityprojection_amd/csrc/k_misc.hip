@@ -260,6 +260,97 @@ __global__ __launch_bounds__(256) void labels_loss_kernel(const float* __restric
   }
 }
 
+// Labels of frames [t0, t0 + 256) of clip b (get_labels, objective.py:40-76,112-139) with the
+// window of VA probabilities staged in LDS: va[t] = sigmoid(vad_logits[t]) computed here exactly as
+// probs_kernel does (so labels equal those of labels_loss_kernel on probs' vad output), then per
+// thread and bit the same sequential fp32 window sum / len >= thr.  The wave-per-frame kernel above
+// issued its window reads from global memory one after another (~57 us per bench step).
+constexpr int LB_T = 256;
+__global__ __launch_bounds__(LB_T) void labels_lds_kernel(const float* __restrict__ vadl, int Tn, int nl, int4 bf,
+                                                          int nb, float thr, int64_t* __restrict__ labels) {
+  __shared__ float sva[2][LB_T + 128];
+  const int b = blockIdx.y, t0 = blockIdx.x * LB_T, tid = threadIdx.x;
+  const int bfr[4] = {bf.x, bf.y, bf.z, bf.w};
+  int hz = 0;
+  for (int i = 0; i < nb; ++i) hz += bfr[i];
+  const int nrow = min(LB_T + hz, Tn - 1 - t0);  // frames t0 + 1 .. used by this block's windows
+  for (int i = tid; i < 2 * nrow; i += LB_T) {
+    const int r = i >> 1, c = i & 1;
+    const float x = vadl[((int64_t)b * Tn + t0 + 1 + r) * 2 + c];
+    sva[c][r] = 1.0f / (1.0f + expf(-x));
+  }
+  __syncthreads();
+  const int t = t0 + tid;
+  if (t >= nl) return;
+  int64_t label = 0;
+  for (int c = 0; c < 2; ++c) {
+    int start = 0;
+    for (int bin = 0; bin < nb; ++bin) {
+      float sm = 0.f;
+      for (int j = 0; j < bfr[bin]; ++j) sm += sva[c][tid + start + j];
+      if ((sm / (float)bfr[bin]) >= thr) label |= (int64_t)1 << (c * nb + bin);
+      start += bfr[bin];
+    }
+  }
+  labels[(int64_t)b * nl + t] = label;
+}
+
+// probs_kernel plus loss_vap (reduction none, objective.py:220-243) of frames t < nl from the
+// labels above: loss = logsumexp(logits) - logits[label], with the softmax's own max / sum
+__global__ __launch_bounds__(256) void probs_loss_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
+                                                        int Tn, int64_t frames, int nb, int now0, int now1, int fut0,
+                                                        int fut1, float* __restrict__ probs, float* __restrict__ vad,
+                                                        float* __restrict__ p_now, float* __restrict__ p_future,
+                                                        float* __restrict__ H, const int64_t* __restrict__ labels,
+                                                        int nl, float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= frames) return;
+  const f32x4 x = *(const f32x4*)(logits + f * 256 + lane * 4);
+  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+  f32x4 e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
+  const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
+  const f32x4 p = e / sum;
+  *(f32x4*)(probs + f * 256 + lane * 4) = p;
+  float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
+  const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
+  const unsigned mfut = ((1u << (fut1 - fut0 + 1)) - 1u) << fut0;
+  const unsigned bm = (1u << nb) - 1u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned k = lane * 4 + i;
+    h += -p[i] * log2f(p[i]);
+    const unsigned k0 = k & bm, k1 = (k >> nb) & bm;
+    n0 += p[i] * (float)__popc(k0 & mnow);
+    n1 += p[i] * (float)__popc(k1 & mnow);
+    u0 += p[i] * (float)__popc(k0 & mfut);
+    u1 += p[i] * (float)__popc(k1 & mfut);
+  }
+  h = wave_sum(h);
+  n0 = wave_sum(n0);
+  n1 = wave_sum(n1);
+  u0 = wave_sum(u0);
+  u1 = wave_sum(u1);
+  if (lane == 0) {
+    H[f] = h;
+    const float dn = n0 + n1 + 1e-5f, du = u0 + u1 + 1e-5f;
+    p_now[f * 2 + 0] = n0 / dn;
+    p_now[f * 2 + 1] = n1 / dn;
+    p_future[f * 2 + 0] = u0 / du;
+    p_future[f * 2 + 1] = u1 / du;
+    vad[f * 2 + 0] = 1.0f / (1.0f + expf(-vadl[f * 2 + 0]));
+    vad[f * 2 + 1] = 1.0f / (1.0f + expf(-vadl[f * 2 + 1]));
+    const int64_t b = f / Tn;
+    const int t = (int)(f - b * Tn);
+    if (t < nl) {
+      const int64_t i = b * nl + t;
+      loss[i] = (mx + logf(sum)) - logits[f * 256 + labels[i]];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict__ probs, int64_t frames, int nb,
                                                        int from_bin, int to_bin, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
@@ -423,6 +514,28 @@ hipError_t launch_labels_loss(const float* logits, const float* va, int B, int T
   const int64_t n = (int64_t)B * nl;
   hipLaunchKernelGGL(labels_loss_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, logits, va, B, Tn, nl, bf,
                      n_bins, threshold, labels, loss);
+  return hipGetLastError();
+}
+
+hipError_t launch_probs_loss(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0,
+                             int now1, int fut0, int fut1, const int* bin_frames, float threshold, float* probs,
+                             float* vad, float* p_now, float* p_future, float* H, int64_t* labels, float* loss,
+                             hipStream_t st) {
+  if (n_bins < 1 || n_bins > 4) return hipErrorInvalidValue;
+  int horizon = 0;
+  int4 bf = {0, 0, 0, 0};
+  int* bp = &bf.x;
+  for (int i = 0; i < n_bins; ++i) {
+    bp[i] = bin_frames[i];
+    horizon += bin_frames[i];
+  }
+  const int nl = Tn - horizon;
+  if (nl <= 0 || horizon > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(labels_lds_kernel, dim3((unsigned)((nl + LB_T - 1) / LB_T), (unsigned)B), dim3(LB_T), 0, st,
+                     vad_logits, Tn, nl, bf, n_bins, threshold, labels);
+  const int64_t frames = (int64_t)B * Tn;
+  hipLaunchKernelGGL(probs_loss_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, logits, vad_logits, Tn,
+                     frames, n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H, labels, nl, loss);
   return hipGetLastError();
 }
 

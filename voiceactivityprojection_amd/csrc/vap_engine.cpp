@@ -878,14 +878,16 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
     ga.gamma = h->P("ar.combinator.ln.weight");
     ga.beta = h->P("ar.combinator.ln.bias");
     HIPCHK(gemm<T>(ga, st, true));
+    // second half + the first's fp32 rows, stored straight in the storage type (the vap_head GEMM's
+    // operand; a separate fp32 -> bf16 pass over HC cost 16 us per bench step)
     GemmArgs gb = ga;
     gb.A = RAW + t1;
     gb.W = h->W<T>("comb_b");
     gb.add = HC;
     gb.ld_add = D;
     gb.add_seq_stride = t1;
-    HIPCHK(gemm<T>(gb, st, true));
-    HIPCHK(launch_layernorm<T>(HC, (int64_t)r.nc * T_, nullptr, nullptr, 0.f, nullptr, HCT, st));
+    gb.C = HCT;
+    HIPCHK(gemm<T>(gb, st, false));
     HIPCHK(gemm<T>(gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
                          logits + r.c0 * (int64_t)T_ * 256, 256, (int64_t)T_ * 256), st, true));
     HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
@@ -2214,6 +2216,25 @@ int vap_probs(const float* logits, const float* vad_logits, int batch, int frame
     return fail(VAP_ERR_INVALID, "bad bin limits");
   HIPCHK(launch_probs(logits, vad_logits, batch, frames, n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H,
                       (hipStream_t)stream));
+  return VAP_OK;
+}
+
+int vap_probs_loss(const float* logits, const float* vad_logits, int batch, int frames, int n_bins, int now0, int now1,
+                   int fut0, int fut1, const int* bin_frames, float threshold, float* probs, float* vad, float* p_now,
+                   float* p_future, float* H, int64_t* labels, float* loss, void* stream) {
+  if (!logits || !vad_logits || !probs || !vad || !p_now || !p_future || !H || !bin_frames || !labels || !loss)
+    return fail(VAP_ERR_INVALID, "null argument");
+  if (n_bins != 4) return fail(VAP_ERR_UNSUPPORTED, "n_bins must be 4");
+  if (now0 < 0 || now1 < now0 || now1 >= n_bins || fut0 < 0 || fut1 < fut0 || fut1 >= n_bins)
+    return fail(VAP_ERR_INVALID, "bad bin limits");
+  int horizon = 0;
+  for (int i = 0; i < n_bins; ++i) horizon += bin_frames[i];
+  if (frames - 1 < horizon)
+    return fail(VAP_ERR_TOO_SHORT, "maximum size for tensor at dimension 1 is " + std::to_string(frames - 1) +
+                                       " but size is " + std::to_string(horizon));
+  if (horizon > 128) return fail(VAP_ERR_UNSUPPORTED, "projection horizon above 128 frames");
+  HIPCHK(launch_probs_loss(logits, vad_logits, batch, frames, n_bins, now0, now1, fut0, fut1, bin_frames, threshold,
+                           probs, vad, p_now, p_future, H, labels, loss, (hipStream_t)stream));
   return VAP_OK;
 }
 

@@ -167,6 +167,12 @@ hipError_t launch_convert_rows(const float* in, int64_t in_seq, T* out, int64_t 
 hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0, int now1,
                         int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,
                         hipStream_t st);
+// probs epilogue + labels + loss in two launches (labels from the VAD logits through LDS, the loss
+// from the softmax's max / sum): what VapGPT.probs needs after the forward
+hipError_t launch_probs_loss(const float* logits, const float* vad_logits, int B, int Tn, int n_bins, int now0,
+                             int now1, int fut0, int fut1, const int* bin_frames, float threshold, float* probs,
+                             float* vad, float* p_now, float* p_future, float* H, int64_t* labels, float* loss,
+                             hipStream_t st);
 hipError_t launch_labels_loss(const float* logits, const float* va, int B, int Tn, const int* bin_frames, int n_bins,
                               float threshold, int64_t* labels, float* loss, hipStream_t st);
 

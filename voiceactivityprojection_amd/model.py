@@ -328,14 +328,20 @@ class VapGPT(nn.Module):
         p_future = torch.empty(B, T, 2, device=dev)
         H = torch.empty(B, T, device=dev)
         st = N.stream_ptr(dev)
-        N.check(N.lib().vap_probs(logits.data_ptr(), vad_logits.data_ptr(), B, T, self.objective.n_bins,
-                                  now_lims[0], now_lims[-1], future_lims[0], future_lims[1], probs.data_ptr(),
-                                  vad.data_ptr(), p_now.data_ptr(), p_future.data_ptr(), H.data_ptr(), st),
-                "vap_probs")
-        ret = {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H}
-        _, loss = self.objective.labels_and_loss(vad, logits)
-        ret["loss"] = loss
-        return ret
+        obj = self.objective
+        if T - 1 < obj.horizon:  # quirk Q2: the reference fails in unfold
+            raise RuntimeError(f"maximum size for tensor at dimension 1 is {T - 1} but size is {obj.horizon}")
+        n = T - obj.horizon
+        labels = torch.empty(B, n, dtype=torch.int64, device=dev)
+        loss = torch.empty(B, n, dtype=torch.float32, device=dev)
+        bf = (ctypes.c_int * obj.n_bins)(*obj.bin_frames)
+        # softmax / sigmoid / H / p_now / p_future, then labels from the model's own sigmoid VAD (quirk Q1)
+        # and loss_vap (objective.py:209-243) in one call
+        N.check(N.lib().vap_probs_loss(logits.data_ptr(), vad_logits.data_ptr(), B, T, obj.n_bins, now_lims[0],
+                                       now_lims[-1], future_lims[0], future_lims[1], bf, obj.threshold_ratio,
+                                       probs.data_ptr(), vad.data_ptr(), p_now.data_ptr(), p_future.data_ptr(),
+                                       H.data_ptr(), labels.data_ptr(), loss.data_ptr(), st), "vap_probs_loss")
+        return {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H, "loss": loss}
 
     @torch.no_grad()
     def vad(self, waveform: Tensor, max_fill_silence_time: float = 0.02, max_omit_spike_time: float = 0.02,
