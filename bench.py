@@ -184,12 +184,12 @@ def main():
         # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
         # by the concurrent LSTM) x the rows of one launch here
         traffic, traffic_src = None, None
-        tp = os.path.join(REPO, "profiles", "r1_traffic_pmc.json")
+        tp = os.path.join(REPO, "profiles", "r2_traffic_pmc.json")  # the current conv01 kernel (v11)
         if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
             per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
             rows_per_launch = 2 * B * L[1] / launches_per_step
             traffic = round(per_row * rows_per_launch / 1e9, 3)
-            traffic_src = "profiles/r1_traffic_pmc.json (GB per launch)"
+            traffic_src = "profiles/r2_traffic_pmc.json (GB per launch)"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "audio-s/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,

@@ -11,7 +11,9 @@ import os
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libvap_hip.so")
+# VAP_LIB_AB=<name> loads _lib/<name> instead (A/B timing of two builds of the engine on one box;
+# the name must be a file in _lib, so the package never loads a library from elsewhere)
+LIB_PATH = os.path.join(_HERE, "_lib", os.path.basename(os.environ.get("VAP_LIB_AB", "")) or "libvap_hip.so")
 
 VAP_OK, VAP_ERR_INVALID, VAP_ERR_TOO_SHORT, VAP_ERR_HIP, VAP_ERR_WEIGHTS, VAP_ERR_UNSUPPORTED = range(6)
 PRECISION = {"fp32": 0, "bf16": 1}

@@ -1208,11 +1208,21 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     }
   }
 
-  f32x16 acc[8];  // [row tile] of C^T (32 channels x 32 rows), in AGPRs
+  // [row tile] of C^T (32 channels x 32 rows), in AGPRs; they start at the conv1 bias (lane element
+  // e: channel 32w + 8(e/4) + 4(lane/32) + e%4), written here with the wait states the first MFMA
+  // reading them as SrcC needs (the MFMAs are inline asm, invisible to the hazard recognizer)
+  f32x16 acc[8];
+  {
+    f32x4 bb[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(EP + w * 32 + 4 * (lane >> 5) + 8 * q);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = bb[e >> 2][e & 3];
+    asm volatile("s_nop 4" : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]));
+    asm volatile("s_nop 4" : "+a"(acc[4]), "+a"(acc[5]), "+a"(acc[6]), "+a"(acc[7]));
+  }
 
   // fragment n = 16h + 8kh + i: tap offset h, k half kh (chunks 2kh + lane/32), row tile i
   auto gread = [&](auto slc, int n) -> chunk16 {
@@ -1273,71 +1283,61 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   unit(30, I0{}, W[0], W[1], false);
   unit(31, I1{}, W[1], W[0], true);
 
-  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[m = i*32 + lane%32][n = 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15
+  // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[m = i*32 + lane%32][n = 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15 (+ b1).
+  // One exchange of per-wave (mean, M2) pairs over the wave's 32 channels (Chan's parallel variance)
+  // through the free G slots; gamma / beta read from LDS per row tile.
 #pragma unroll
   for (int i = 0; i < 8; i += 4)  // MFMA -> VALU read of the accumulators
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
                  : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slots
   const int cb = w * 32 + 4 * (lane >> 5);  // channel of e = 0; e -> cb + 8(e/4) + e%4
-  f32x4 bb[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(EP + cb + 8 * q);
+  float2* red2 = (float2*)G;                // [256 rows][8 waves] (mean, M2)
   auto val = [&](int i, int q) -> f32x4 {
-    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]} + bb[q];
+    return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
+  };
+  auto xsum = [](float x) {  // x + x of lane ^ 32
+    float a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+    return a + b;
   };
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
     const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
-    float sum = (t[0] + t[1]) + (t[2] + t[3]);
-    sum += __shfl_xor(sum, 32, 64);
-    if (lane < 32) red[(i * 32 + lane) * 8 + w] = sum;
-  }
-  __syncthreads();
-  float mean[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
-    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
-    mean[i] = ((pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]))) * (1.0f / BN);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    const float mw = xsum((t[0] + t[1]) + (t[2] + t[3])) * (1.0f / 32);
+    f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 d = val(i, q) - mean[i];
-      t += d * d;
+      const f32x4 d = val(i, q) - mw;
+      d2 += d * d;
     }
-    float ss = (t[0] + t[1]) + (t[2] + t[3]);
-    ss += __shfl_xor(ss, 32, 64);
-    if (lane < 32) red[(i * 32 + lane) * 8 + w] = ss;
+    const float m2 = xsum((d2[0] + d2[1]) + (d2[2] + d2[3]));
+    if (lane < 32) red2[(i * 32 + lane) * 8 + w] = float2{mw, m2};
   }
-  __syncthreads();
-  f32x4 gg[4], ee[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    gg[q] = *(const f32x4*)(EP + 256 + cb + 8 * q);
-    ee[q] = *(const f32x4*)(EP + 512 + cb + 8 * q);
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // 16-B stores: for channel blocks (2p, 2p+1) one v_permlane32_swap per dword gives lanes 0-31 the
   // 8 channels of block 2p and lanes 32-63 those of block 2p+1
   bf16* obase = out + (int64_t)s * out_seq_stride;
   const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const f32x4 pa = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8);
-    const f32x4 pb = *(const f32x4*)(red + (i * 32 + (lane & 31)) * 8 + 4);
-    const float var = (pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
-    const float rstd = rsqrtf(var * (1.0f / (BN - 1)) + 1e-5f);
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4* rp = (const f32x4*)(red2 + (i * 32 + (lane & 31)) * 8);
+    const f32x4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
+    const float mean = (((q0[0] + q0[2]) + (q1[0] + q1[2])) + ((q2[0] + q2[2]) + (q3[0] + q3[2]))) * 0.125f;
+    auto dev = [&](float mw) { return (mw - mean) * (mw - mean); };
+    const float M2 = (((q0[1] + q0[3]) + (q1[1] + q1[3])) + ((q2[1] + q2[3]) + (q3[1] + q3[3]))) +
+                     32.0f * (((dev(q0[0]) + dev(q0[2])) + (dev(q1[0]) + dev(q1[2]))) +
+                              ((dev(q2[0]) + dev(q2[2])) + (dev(q3[0]) + dev(q3[2]))));
+    const float rstd = rsqrtf(M2 * (1.0f / (BN - 1)) + 1e-5f);
     const int t = t0 + i * 32 + (lane & 31);
     uint32_t pk[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 v = (val(i, q) - mean[i]) * rstd * gg[q] + ee[q];
+      const f32x4 gg = *(const f32x4*)(EP + 256 + cb + 8 * q), ee = *(const f32x4*)(EP + 512 + cb + 8 * q);
+      const f32x4 v = (val(i, q) - mean) * rstd * gg + ee;
       pk[q][0] = relu_bf16x2(v[0], v[1]);
       pk[q][1] = relu_bf16x2(v[2], v[3]);
     }
