@@ -377,3 +377,29 @@ def test_lnproj_fused(M, mode):
         refr = x.to(torch.bfloat16).float() @ Wr.float().t()
         errr = (cr.float().cpu() - refr).abs().max().item()
         assert errr <= 1e-2 * max(1.0, refr.abs().max().item()), f"cr M={M}: {errr}"
+
+
+@pytest.mark.parametrize("B,T", [(1, 37), (2, 1000), (3, 129)])
+def test_heads_fused(B, T):
+    """Fused combinator + vap_head (k_block.hip heads_kernel): logits = (GELU(LN(x1 Wa^T)) +
+    GELU(LN(x2 Wb^T))) Wh^T + bh with one shared LayerNorm (modules.py:434-449, model.py:257-261),
+    against the torch fp32 composition on the same bf16 operands (h rounded to bf16 as the kernel
+    feeds it to the head GEMM; the kernel's GELU is the sigmoid fit, |error| <= 2.7e-4)."""
+    L = lib()
+    D = 256
+    g = torch.Generator().manual_seed(31 + B * T)
+    x = (torch.randn(2 * B, T, D, generator=g) * 1.5).to(torch.bfloat16)
+    Wa, Wb, Wh = [(torch.randn(D, D, generator=g) / 16).to(torch.bfloat16) for _ in range(3)]
+    ga = 1 + 0.2 * torch.randn(D, generator=g)
+    be = 0.1 * torch.randn(D, generator=g)
+    hb = 0.1 * torch.randn(D, generator=g)
+    out = torch.full((B, T, D), 7.0, device="cuda")
+    d = [t.cuda() for t in (x, Wa, Wb, Wh, ga, be, hb)]
+    _run(L.lib().vap_test_heads, _p(d[0]), B, T, _p(d[1]), _p(d[2]), _p(d[3]), _p(d[4]), _p(d[5]), _p(d[6]), _p(out),
+         _st())
+    xf = x.float().view(B, 2, T, D)
+    h = F.gelu(F.layer_norm(xf[:, 0] @ Wa.float().t(), (D,), ga, be)) + \
+        F.gelu(F.layer_norm(xf[:, 1] @ Wb.float().t(), (D,), ga, be))
+    ref = h.to(torch.bfloat16).float() @ Wh.float().t() + hb
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 1e-2 * max(1.0, ref.abs().max().item()), f"heads B={B} T={T}: {err}"

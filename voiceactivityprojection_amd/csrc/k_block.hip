@@ -616,6 +616,185 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Combinator + vap_head of 64 frames in one launch (bf16 path; modules.py:434-449, model.py:257-261):
+//   h      = GELU(LN(x1 . Wa^T)) + GELU(LN(x2 . Wb^T))      (one shared LayerNorm, no biases)
+//   logits = h . Wh^T + bh
+// x1 / x2 are the two speakers' rows of the bf16 copy of x the last layer's block kernel writes.
+// Same row-block structure as block_kernel (8 waves, wave w owns output columns 32w .. +31 of all
+// 64 rows, weights streamed from L2 in the packed row-panel layout, A panels in LDS): both panels
+// are loaded at once, h stays in registers between the two halves and reaches LDS once, as the
+// head's A panel.  Replaces two LN+GELU GEMM launches and the head GEMM (43 + 56 + 26 us per step).
+// ------------------------------------------------------------------------------------------
+template <int MT>
+__global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
+  constexpr int R = 16 * MT;
+  constexpr int NQ = 24, NPF = 2;  // Wa 8 + Wb 8 + Wh 8 k-steps
+  constexpr int OFF_P = R * ROWB, OFF_RED = 2 * R * ROWB, OFF_GB = OFF_RED + 2 * R * 8 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_GB + 3 * D * 4];
+  unsigned char* H = smem;          // x1 panel, then h
+  unsigned char* P = smem + OFF_P;  // x2 panel
+  float* red0 = (float*)(smem + OFF_RED);
+  float* red1 = red0 + R * 8;
+  float* GB = (float*)(smem + OFF_GB);  // gamma | beta | head bias
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * R;
+
+  // frame m -> clip m / T, t = m % T; x1 row = clip's sequence 2c, x2 row = 2c + 1 (+ x_seq)
+  const int64_t xbase = (int64_t)(m0 / g.T) * 2 * g.x_seq + (int64_t)(m0 % g.T) * D;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
+  constexpr int OPT = R * 32 / 512;  // 16-B chunks per thread and panel
+  chunk16 a1[OPT], a2[OPT];
+  {
+    uint32_t oo[OPT];
+    rows16_off(m0 + (tid >> 5), g.M, g.T, 2 * g.x_seq, D, xbase, 2, oo, OPT);
+#pragma unroll
+    for (int k = 0; k < OPT; ++k) {
+      a1[k] = buf_load16(rx, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+      a2[k] = buf_load16(rx, oo[k] == 0x80000000u ? oo[k] : oo[k] + (uint32_t)(g.x_seq * 2 + (tid & 31) * 16), 0);
+    }
+  }
+  f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 192) gbv = *(const f32x4*)((tid < 64 ? g.gamma : tid < 128 ? g.beta : g.hbias) + (tid & 63) * 4);
+
+  auto wload = [&](int q, chunk16* r) {  // q static after unrolling
+    const bf16* base = q < 8 ? g.Wa : q < 16 ? g.Wb : g.Wh;
+    const int kidx = q & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+  };
+  chunk16 wr[NPF][2];
+#pragma unroll
+  for (int p = 0; p < NPF; ++p) wload(p, wr[p]);
+  const uint32_t afo = (uint32_t)(l16 * ROWB + (lg ^ l16) * 16);
+  auto kstep = [&](const unsigned char* img, int ks, int q, f32x4 (&c)[2][MT]) {
+    chunk16 af[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) af[j] = *(const chunk16*)(img + j * 16 * ROWB + (afo ^ (uint32_t)(ks * 64)));
+    chunk16* wf = wr[q % NPF];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) c[i][j] = mfma_chunk<bf16>(wf[i], af[j], c[i][j]);
+    wload(q + NPF < NQ ? q + NPF : NQ - 1, wf);  // unconditional (see block_kernel)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+#pragma unroll
+  for (int k = 0; k < OPT; ++k) {
+    const int id = tid + k * 512, row = id >> 5, c = id & 31;
+    *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = a1[k];
+    *(chunk16*)(P + row * ROWB + xswz(row, c) * 16) = a2[k];
+  }
+  if (tid < 192) *(f32x4*)(GB + tid * 4) = gbv;
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);  // phases apart (mixed by the scheduler they held 178 VGPRs)
+
+  auto gsum = [](float v) {  // sum over the 4 16-lane groups (inline asm: see ln_panel)
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    float c = a + b, d = c;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+    return c + d;
+  };
+  auto rowtot = [&](const float* red, int j) {
+    const f32x4 a = *(const f32x4*)(red + (j * 16 + l16) * 8), b = *(const f32x4*)(red + (j * 16 + l16) * 8 + 4);
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+  };
+  // GELU(LayerNorm(c)) of the rows (shared combinator LN, biased variance), accumulated into h
+  auto ln_gelu = [&](const f32x4 (&c)[2][MT], f32x4 (&h)[2][MT], bool first) {
+    float mean[MT], rstd[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) sm += (c[i][j][0] + c[i][j][1]) + (c[i][j][2] + c[i][j][3]);
+      red0[(j * 16 + l16) * 8 + w] = gsum(sm);
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      mean[j] = rowtot(red0, j) * (1.0f / D);
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = c[i][j][e] - mean[j];
+          sm += d * d;
+        }
+      red1[(j * 16 + l16) * 8 + w] = gsum(sm);
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) rstd[j] = rsqrtf(rowtot(red1, j) * (1.0f / D) + g.eps);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = w * 32 + i * 16 + lg * 4;
+      const f32x4 ga = *(const f32x4*)(GB + n), be = *(const f32x4*)(GB + 256 + n);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const f32x4 y = (c[i][j] - mean[j]) * rstd[j] * ga + be;
+        const f32x4 gy = {gelu_sig(y[0]), gelu_sig(y[1]), gelu_sig(y[2]), gelu_sig(y[3])};
+        h[i][j] = first ? gy : h[i][j] + gy;
+      }
+    }
+  };
+
+  f32x4 acc[2][MT], h[2][MT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kstep(H, ks, ks, acc);  // x1 . Wa^T
+  __builtin_amdgcn_sched_barrier(0);
+  ln_gelu(acc, h, true);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kstep(P, ks, 8 + ks, acc);  // x2 . Wb^T
+  __builtin_amdgcn_sched_barrier(0);
+  ln_gelu(acc, h, false);
+  __builtin_amdgcn_sched_barrier(0);
+  // h -> bf16 panel (H: every wave finished its x1 k-steps before the LayerNorms' barriers)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n = w * 32 + i * 16 + lg * 4;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int row = j * 16 + l16;
+      *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
+          pack_bf16x4(h[i][j][0], h[i][j][1], h[i][j][2], h[i][j][3]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const f32x4 hb = *(const f32x4*)(GB + 512 + w * 32 + i * 16 + lg * 4);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = hb;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) kstep(H, ks, 16 + ks, acc);  // h . Wh^T + bh
+  // logits rows m (contiguous [M][256] fp32)
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(g.logits + (int64_t)m0 * D, 0x7FFFFFF0u);
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int m = m0 + j * 16 + l16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      buf_store16(rl, m < g.M ? (uint32_t)(((j * 16 + l16) * D + w * 32 + i * 16 + lg * 4) * 4) : 0x80000000u,
+                  __builtin_bit_cast(u32x4, acc[i][j]));
+  }
+}
 }  // namespace
 
 // supported: (o, np 1, nr 0) out-proj + LN + cross Q; (no o, np 3, nr 0) LN + QKV; (no o, np 3, nr 2)
@@ -636,4 +815,12 @@ hipError_t launch_lnproj(const LnProjArgs& g, hipStream_t st) {
 
 hipError_t read_lnproj_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lnp_stamps), sizeof(g_lnp_stamps), 0, hipMemcpyDeviceToHost);
+}
+
+hipError_t launch_heads(const HeadsArgs& g, hipStream_t st) {
+  if (g.M <= 0 || g.T <= 0 || !g.x || !g.Wa || !g.Wb || !g.Wh || !g.logits || g.x_seq % 8) return hipErrorInvalidValue;
+  // a workgroup's rows lie within the 2 GiB a buffer offset reaches from its first row
+  if ((64 / g.T + 2) * 2 * g.x_seq * 2 + 64 * D * 2 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((heads_kernel<4>), dim3((g.M + 63) / 64), dim3(512), 0, st, g);
+  return hipGetLastError();
 }

@@ -79,6 +79,7 @@ struct vap_handle {
   // forwards without per-launch timing events; one stream keeps each kernel's events clean)
   hipStream_t fe_stream = nullptr;
   int fe_streams = 1;
+  bool heads_fused = true;  // VAP_HEADS_FUSED=0: combinator + vap_head as three GEMM launches
   bool fe_first_serial = false;
   int fe_gate = 0;  // VAP_FE_GATE: see conv_rows
   bool fe_align = true;  // VAP_FE_ALIGN=0: conv1..3 ranges per piece exactly what its conv4 rows need
@@ -562,8 +563,10 @@ int pack_all(vap_handle* h, hipStream_t st) {
   if (!h->dims.mono) {
     if ((rc = cat("comb_a", {"ar.combinator.h0_a.weight"}))) return rc;
     if ((rc = cat("comb_b", {"ar.combinator.h0_b.weight"}))) return rc;
+    if ((rc = rp_copy("comb_a", D)) || (rc = rp_copy("comb_b", D))) return rc;  // fused heads (k_block.hip)
   }
   if ((rc = cat("head", {"vap_head.weight"}))) return rc;
+  if (!h->dims.mono && (rc = rp_copy("head", 256))) return rc;
   return VAP_OK;
 }
 
@@ -868,6 +871,19 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
   }
   float* HC = (float*)(ws + p.HC) + r.c0 * t1;
   T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
+  if constexpr (sizeof(T) == 2) {
+    if (h->heads_fused) {  // combinator + vap_head in one launch (k_block.hip heads_kernel)
+      Timed tm(h, VAP_K_HEADS, st);
+      if (!raw_ready) HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
+      HeadsArgs ha{(const bf16*)RAW, t1, r.nc * T_, T_, (const bf16*)h->W<T>("comb_a@rp"), (const bf16*)h->W<T>("comb_b@rp"),
+                   (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"), h->P("ar.combinator.ln.bias"),
+                   h->P("vap_head.bias"), logits + r.c0 * (int64_t)T_ * 256, 1e-5f};
+      HIPCHK(launch_heads(ha, st));
+      HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
+                             vadl + r.c0 * (int64_t)T_ * 2, st));
+      return VAP_OK;
+    }
+  }
   {
     Timed tm(h, VAP_K_HEADS, st);
     if (!raw_ready) HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
@@ -1896,6 +1912,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_FE_ALIGN")) h->fe_align = atoi(e) != 0;
   if (const char* e = getenv("VAP_FE_FIRST_SERIAL")) h->fe_first_serial = atoi(e) != 0;
   if (const char* e = getenv("VAP_FE_GATE")) h->fe_gate = atoi(e);
+  if (const char* e = getenv("VAP_HEADS_FUSED")) h->heads_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);

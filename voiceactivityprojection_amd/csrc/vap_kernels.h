@@ -264,6 +264,24 @@ struct BlockArgs {
   bf16* xb = nullptr;  // optional bf16 copy of the output rows (same row layout as x)
 };
 hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st);
+// combinator + vap_head in one launch (k_block.hip heads_kernel): logits [M][256] fp32 of frames
+// m = clip * T + t from the bf16 rows x of sequences 2 clip / 2 clip + 1 (row t at x + s x_seq + t 256);
+// Wa / Wb / Wh in the packed row-panel layout
+struct HeadsArgs {
+  const bf16* x;
+  int64_t x_seq;
+  int M;  // clips x T
+  int T;
+  const bf16* Wa;
+  const bf16* Wb;
+  const bf16* Wh;
+  const float* gamma;
+  const float* beta;
+  const float* hbias;
+  float* logits;
+  float eps;
+};
+hipError_t launch_heads(const HeadsArgs& g, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);
 // LayerNorm'd projections of a layer in one launch (k_block.hip): with o, x' = x + o . Wo^T is stored
 // to x and cp = LN(x') . Wp^T; without, cp = LN(x) . Wp^T and (nr > 0) cr = x . Wr^T from the raw

@@ -222,6 +222,24 @@ int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W
   (void)hipFree(p);
   return rc_of(e);
 }
+// fused combinator + vap_head (k_block.hip heads_kernel): x bf16 [2 B][T][256] (sequence 2b / 2b + 1 =
+// speaker 0 / 1 of clip b), plain [256][256] bf16 Wa / Wb / Wh -> logits [B][T][256] fp32
+int vap_test_heads(const void* x, int B, int T, const void* Wa, const void* Wb, const void* Wh, const float* gamma,
+                   const float* beta, const float* hbias, float* logits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  void* p = nullptr;
+  const size_t n0 = 256 * 256;
+  if (hipMalloc(&p, 3 * n0 * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+  bf16 *pa = (bf16*)p, *pb = pa + n0, *ph = pb + n0;
+  hipError_t e = launch_pack_rowpanel((const bf16*)Wa, pa, 256, 256, st);
+  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)Wb, pb, 256, 256, st);
+  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)Wh, ph, 256, 256, st);
+  HeadsArgs g{(const bf16*)x, (int64_t)T * 256, B * T, T, pa, pb, ph, gamma, beta, hbias, logits, 1e-5f};
+  if (e == hipSuccess) e = launch_heads(g, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(p);
+  return rc_of(e);
+}
 int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
                           const float* gamma, const float* beta, int cus, void* stream) {
   BlockArgs g{x, (const bf16*)o, M, 0, 0, 0, Wop, W1p, W2p, gamma, beta, 1e-5f};
