@@ -217,9 +217,10 @@ int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* 
                     void* cp, void* cr, const float* gamma, const float* beta, void* stream);
 /* fused combinator + vap_head (bf16 path, k_block.hip heads_kernel): x bf16 [2B][T][256] (sequences 2b / 2b+1 =
  * the two speakers of clip b), plain [256][256] bf16 Wa / Wb / Wh -> logits [B][T][256] fp32 =
- * (GELU(LN(x1 Wa^T)) + GELU(LN(x2 Wb^T))) Wh^T + hbias */
+ * (GELU(LN(x1 Wa^T)) + GELU(LN(x2 Wb^T))) Wh^T + hbias, vad [B][T][2] = x1 / x2 . vw + vb */
 int vap_test_heads(const void* x, int B, int T, const void* Wa, const void* Wb, const void* Wh, const float* gamma,
-                   const float* beta, const float* hbias, float* logits, void* stream);
+                   const float* beta, const float* hbias, const float* vw, const float* vb, float* logits, float* vad,
+                   void* stream);
 /* the same with weights already packed (vap_test_pack_weight) */
 int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const void* W1p, const void* W2p,
                           const float* gamma, const float* beta, int cus, void* stream);

@@ -393,10 +393,16 @@ def test_heads_fused(B, T):
     ga = 1 + 0.2 * torch.randn(D, generator=g)
     be = 0.1 * torch.randn(D, generator=g)
     hb = 0.1 * torch.randn(D, generator=g)
+    vw = 0.05 * torch.randn(D, generator=g)
+    vb = 0.1 * torch.randn(1, generator=g)
     out = torch.full((B, T, D), 7.0, device="cuda")
-    d = [t.cuda() for t in (x, Wa, Wb, Wh, ga, be, hb)]
-    _run(L.lib().vap_test_heads, _p(d[0]), B, T, _p(d[1]), _p(d[2]), _p(d[3]), _p(d[4]), _p(d[5]), _p(d[6]), _p(out),
-         _st())
+    vad = torch.full((B, T, 2), 7.0, device="cuda")
+    d = [t.cuda() for t in (x, Wa, Wb, Wh, ga, be, hb, vw, vb)]
+    _run(L.lib().vap_test_heads, _p(d[0]), B, T, _p(d[1]), _p(d[2]), _p(d[3]), _p(d[4]), _p(d[5]), _p(d[6]), _p(d[7]),
+         _p(d[8]), _p(out), _p(vad), _st())
+    vref = (x.float().view(B, 2, T, D) @ vw + vb).permute(0, 2, 1)
+    verr = (vad.cpu() - vref).abs().max().item()
+    assert verr <= 1e-4 * max(1.0, vref.abs().max().item()), f"heads vad B={B} T={T}: {verr}"
     xf = x.float().view(B, 2, T, D)
     h = F.gelu(F.layer_norm(xf[:, 0] @ Wa.float().t(), (D,), ga, be)) + \
         F.gelu(F.layer_norm(xf[:, 1] @ Wb.float().t(), (D,), ga, be))

@@ -84,7 +84,7 @@ _SIGS = {
     "vap_test_read_lnproj_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_gemm_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_lstm_stamps": (ctypes.c_int, [_P]),
-    "vap_test_heads": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "vap_test_heads": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vap_test_read_lstm_handoff": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),

@@ -618,7 +618,8 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
 
 
 // ------------------------------------------------------------------------------------------
-// Combinator + vap_head of 64 frames in one launch (bf16 path; modules.py:434-449, model.py:257-261):
+// Combinator + vap_head (+ va_classifier) of 64 frames in one launch (bf16 path; modules.py:434-449,
+// model.py:257-261; the VAD logits from the same bf16 rows):
 //   h      = GELU(LN(x1 . Wa^T)) + GELU(LN(x2 . Wb^T))      (one shared LayerNorm, no biases)
 //   logits = h . Wh^T + bh
 // x1 / x2 are the two speakers' rows of the bf16 copy of x the last layer's block kernel writes.
@@ -632,12 +633,12 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
   constexpr int R = 16 * MT;
   constexpr int NQ = 24, NPF = 2;  // Wa 8 + Wb 8 + Wh 8 k-steps
   constexpr int OFF_P = R * ROWB, OFF_RED = 2 * R * ROWB, OFF_GB = OFF_RED + 2 * R * 8 * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_GB + 3 * D * 4];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[OFF_GB + 4 * D * 4];
   unsigned char* H = smem;          // x1 panel, then h
   unsigned char* P = smem + OFF_P;  // x2 panel
   float* red0 = (float*)(smem + OFF_RED);
   float* red1 = red0 + R * 8;
-  float* GB = (float*)(smem + OFF_GB);  // gamma | beta | head bias
+  float* GB = (float*)(smem + OFF_GB);  // gamma | beta | head bias | VAD head weight
   const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = blockIdx.x * R;
@@ -657,7 +658,8 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
     }
   }
   f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
-  if (tid < 192) gbv = *(const f32x4*)((tid < 64 ? g.gamma : tid < 128 ? g.beta : g.hbias) + (tid & 63) * 4);
+  if (tid < 256)
+    gbv = *(const f32x4*)((tid < 64 ? g.gamma : tid < 128 ? g.beta : tid < 192 ? g.hbias : g.vw) + (tid & 63) * 4);
 
   auto wload = [&](int q, chunk16* r) {  // q static after unrolling
     const bf16* base = q < 8 ? g.Wa : q < 16 ? g.Wb : g.Wh;
@@ -688,8 +690,25 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
     *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = a1[k];
     *(chunk16*)(P + row * ROWB + xswz(row, c) * 16) = a2[k];
   }
-  if (tid < 192) *(f32x4*)(GB + tid * 4) = gbv;
+  if (tid < 256) *(f32x4*)(GB + tid * 4) = gbv;
   __syncthreads();
+  {  // va_classifier (model.py:257-259) of both speakers from the panels: 4 threads per (row, speaker)
+    const int r = tid >> 3, sp = (tid >> 2) & 1, part = tid & 3;
+    const unsigned char* img = sp ? P : H;
+    float dsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = part * 8 + k;
+      const bf16x8 v = *(const bf16x8*)(img + r * ROWB + xswz(r, c) * 16);
+      const f32x4 w0 = *(const f32x4*)(GB + 768 + c * 8), w1 = *(const f32x4*)(GB + 768 + c * 8 + 4);
+      dsum += (((float)v[0] * w0[0] + (float)v[1] * w0[1]) + ((float)v[2] * w0[2] + (float)v[3] * w0[3])) +
+              (((float)v[4] * w1[0] + (float)v[5] * w1[1]) + ((float)v[6] * w1[2] + (float)v[7] * w1[3]));
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    dsum += __shfl_xor(dsum, 2, 64);
+    const int m = m0 + r;
+    if (part == 0 && m < g.M) g.vad[(int64_t)m * 2 + sp] = dsum + g.vb[0];
+  }
   __builtin_amdgcn_sched_barrier(0);  // phases apart (mixed by the scheduler they held 178 VGPRs)
 
   auto gsum = [](float v) {  // sum over the 4 16-lane groups (inline asm: see ln_panel)
@@ -818,7 +837,8 @@ hipError_t read_lnproj_stamps(unsigned long long* out) {
 }
 
 hipError_t launch_heads(const HeadsArgs& g, hipStream_t st) {
-  if (g.M <= 0 || g.T <= 0 || !g.x || !g.Wa || !g.Wb || !g.Wh || !g.logits || g.x_seq % 8) return hipErrorInvalidValue;
+  if (g.M <= 0 || g.T <= 0 || !g.x || !g.Wa || !g.Wb || !g.Wh || !g.logits || !g.vw || !g.vb || !g.vad || g.x_seq % 8)
+    return hipErrorInvalidValue;
   // a workgroup's rows lie within the 2 GiB a buffer offset reaches from its first row
   if ((64 / g.T + 2) * 2 * g.x_seq * 2 + 64 * D * 2 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
   hipLaunchKernelGGL((heads_kernel<4>), dim3((g.M + 63) / 64), dim3(512), 0, st, g);

@@ -877,10 +877,9 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
       if (!raw_ready) HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
       HeadsArgs ha{(const bf16*)RAW, t1, r.nc * T_, T_, (const bf16*)h->W<T>("comb_a@rp"), (const bf16*)h->W<T>("comb_b@rp"),
                    (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"), h->P("ar.combinator.ln.bias"),
-                   h->P("vap_head.bias"), logits + r.c0 * (int64_t)T_ * 256, 1e-5f};
+                   h->P("vap_head.bias"), logits + r.c0 * (int64_t)T_ * 256, 1e-5f, h->P("va_classifier.weight"),
+                   h->P("va_classifier.bias"), vadl + r.c0 * (int64_t)T_ * 2};
       HIPCHK(launch_heads(ha, st));
-      HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
-                             vadl + r.c0 * (int64_t)T_ * 2, st));
       return VAP_OK;
     }
   }

@@ -280,6 +280,9 @@ struct HeadsArgs {
   const float* hbias;
   float* logits;
   float eps;
+  const float* vw;  // va_classifier weight [256] / bias [1] -> vad logits [M][2] (speaker 0 / 1)
+  const float* vb;
+  float* vad;
 };
 hipError_t launch_heads(const HeadsArgs& g, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);

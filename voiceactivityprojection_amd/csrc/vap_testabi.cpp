@@ -225,7 +225,8 @@ int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W
 // fused combinator + vap_head (k_block.hip heads_kernel): x bf16 [2 B][T][256] (sequence 2b / 2b + 1 =
 // speaker 0 / 1 of clip b), plain [256][256] bf16 Wa / Wb / Wh -> logits [B][T][256] fp32
 int vap_test_heads(const void* x, int B, int T, const void* Wa, const void* Wb, const void* Wh, const float* gamma,
-                   const float* beta, const float* hbias, float* logits, void* stream) {
+                   const float* beta, const float* hbias, const float* vw, const float* vb, float* logits, float* vad,
+                   void* stream) {
   hipStream_t st = (hipStream_t)stream;
   void* p = nullptr;
   const size_t n0 = 256 * 256;
@@ -234,7 +235,7 @@ int vap_test_heads(const void* x, int B, int T, const void* Wa, const void* Wb, 
   hipError_t e = launch_pack_rowpanel((const bf16*)Wa, pa, 256, 256, st);
   if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)Wb, pb, 256, 256, st);
   if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)Wh, ph, 256, 256, st);
-  HeadsArgs g{(const bf16*)x, (int64_t)T * 256, B * T, T, pa, pb, ph, gamma, beta, hbias, logits, 1e-5f};
+  HeadsArgs g{(const bf16*)x, (int64_t)T * 256, B * T, T, pa, pb, ph, gamma, beta, hbias, logits, 1e-5f, vw, vb, vad};
   if (e == hipSuccess) e = launch_heads(g, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   (void)hipFree(p);
