@@ -103,3 +103,15 @@ def test_stream_above_cap_recomputes(monkeypatch):
         ref = m(win)
         assert torch.equal(out["logits"], ref["logits"]), k
     st.synchronize()
+
+
+def test_heads_per_chunk_equals_once(monkeypatch):
+    """VAP_HEADS_CHUNKED=1 runs the fused heads kernel per back-end time chunk (frame ranges of every
+    clip) instead of once after the last chunk.  The heads are row-wise, so every output is
+    bit-identical to the default schedule.  20 s clips: chunks of 640 and 360 frames."""
+    w = _batch(3, 320000, 900)
+    ref = _model().probs(w)
+    monkeypatch.setenv("VAP_HEADS_CHUNKED", "1")
+    out = _model().probs(w)
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k

@@ -707,7 +707,8 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
     dsum += __shfl_xor(dsum, 1, 64);
     dsum += __shfl_xor(dsum, 2, 64);
     const int m = m0 + r;
-    if (part == 0 && m < g.M) g.vad[(int64_t)m * 2 + sp] = dsum + g.vb[0];
+    const int64_t om = g.out_T ? (int64_t)(m / g.T) * g.out_T + g.out_f0 + m % g.T : m;
+    if (part == 0 && m < g.M) g.vad[om * 2 + sp] = dsum + g.vb[0];
   }
   __builtin_amdgcn_sched_barrier(0);  // phases apart (mixed by the scheduler they held 178 VGPRs)
 
@@ -803,6 +804,18 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
   }
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) kstep(H, ks, 16 + ks, acc);  // h . Wh^T + bh
+  if (g.out_T) {  // a frame range of every clip: rows clip * out_T + out_f0 + t
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = m0 + j * 16 + l16;
+      if (m < g.M) {
+        float* lr = g.logits + ((int64_t)(m / g.T) * g.out_T + g.out_f0 + m % g.T) * D + w * 32 + lg * 4;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) *(f32x4*)(lr + i * 16) = acc[i][j];
+      }
+    }
+    return;
+  }
   // logits rows m (contiguous [M][256] fp32)
   const __amdgpu_buffer_rsrc_t rl = make_rsrc(g.logits + (int64_t)m0 * D, 0x7FFFFFF0u);
 #pragma unroll
@@ -837,7 +850,7 @@ hipError_t read_lnproj_stamps(unsigned long long* out) {
 }
 
 hipError_t launch_heads(const HeadsArgs& g, hipStream_t st) {
-  if (g.M <= 0 || g.T <= 0 || !g.x || !g.Wa || !g.Wb || !g.Wh || !g.logits || !g.vw || !g.vb || !g.vad || g.x_seq % 8)
+  if (g.M <= 0 || g.T <= 0 || g.out_T < 0 || (g.out_T && g.out_f0 + g.T > g.out_T) || g.out_f0 < 0 || !g.x || !g.Wa || !g.Wb || !g.Wh || !g.logits || !g.vw || !g.vb || !g.vad || g.x_seq % 8)
     return hipErrorInvalidValue;
   // a workgroup's rows lie within the 2 GiB a buffer offset reaches from its first row
   if ((64 / g.T + 2) * 2 * g.x_seq * 2 + 64 * D * 2 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;

@@ -1265,6 +1265,14 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
   T* HCT = (T*)(ws + p.HCT);
   Timed tm(h, VAP_K_HEADS, st);
   const int64_t o = (int64_t)f0 * D;
+  if (h->heads_fused) {  // heads_kernel on the frame range [f0, f0 + nf) of every clip
+    HeadsArgs ha{(const bf16*)(RAW + o), t1, B * nf, nf, (const bf16*)h->W<T>("comb_a@rp"),
+                 (const bf16*)h->W<T>("comb_b@rp"), (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"),
+                 h->P("ar.combinator.ln.bias"), h->P("vap_head.bias"), logits, 1e-5f, h->P("va_classifier.weight"),
+                 h->P("va_classifier.bias"), vadl, T_, f0};
+    HIPCHK(launch_heads(ha, st));
+    return VAP_OK;
+  }
   GemmArgs ga = gargs(RAW + o, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, nf, B, HC + o, D, t1);
   ga.norm = 2;
   ga.act = 2;

@@ -283,6 +283,8 @@ struct HeadsArgs {
   const float* vw;  // va_classifier weight [256] / bias [1] -> vad logits [M][2] (speaker 0 / 1)
   const float* vb;
   float* vad;
+  int out_T = 0;   // frames per clip of logits / vad (0: T); a frame range's rows go to clip * out_T + out_f0 + t
+  int out_f0 = 0;
 };
 hipError_t launch_heads(const HeadsArgs& g, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);
