@@ -1051,6 +1051,11 @@ __global__ __launch_bounds__(512, 1) void conv01k_kernel(const float* __restrict
 // ------------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VAP_DEV int gphys(int row, int c) { return (c + (row >> 2)) & 3; }
+VAP_DEV int c1_lane() {  // the lane id by volatile asm: values derived from it are not hoisted
+  int ln;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+  return ln;
+}
 VAP_DEV void mfma32_acc(f32x16& c, const chunk16& a, const chunk16& b) {
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
@@ -1292,7 +1297,8 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
                  : "+a"(acc[i]), "+a"(acc[i + 1]), "+a"(acc[i + 2]), "+a"(acc[i + 3]));
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slots
-  const int cb = w * 32 + 4 * (lane >> 5);  // channel of e = 0; e -> cb + 8(e/4) + e%4
+  // lane-derived offsets are rebuilt per row tile from a volatile lane read: hoisted, they were
+  // spilled in the prologue and every reload's vmcnt(0) waited for the previous row tile's stores
   float2* red2 = (float2*)G;                // [256 rows][8 waves] (mean, M2)
   auto val = [&](int i, int q) -> f32x4 {
     return f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
@@ -1314,7 +1320,8 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
       d2 += d * d;
     }
     const float m2 = xsum((d2[0] + d2[1]) + (d2[2] + d2[3]));
-    if (lane < 32) red2[(i * 32 + lane) * 8 + w] = float2{mw, m2};
+    const int ln = c1_lane();
+    if (ln < 32) red2[(i * 32 + ln) * 8 + w] = float2{mw, m2};
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // 16-B stores: for channel blocks (2p, 2p+1) one v_permlane32_swap per dword gives lanes 0-31 the
@@ -1324,7 +1331,9 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     __builtin_amdgcn_sched_barrier(0);
-    const f32x4* rp = (const f32x4*)(red2 + (i * 32 + (lane & 31)) * 8);
+    const int ln = c1_lane();
+    const int cb = w * 32 + 4 * (ln >> 5);  // channel of e = 0; e -> cb + 8(e/4) + e%4
+    const f32x4* rp = (const f32x4*)(red2 + (i * 32 + (ln & 31)) * 8);
     const f32x4 q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
     const float mean = (((q0[0] + q0[2]) + (q1[0] + q1[2])) + ((q2[0] + q2[2]) + (q3[0] + q3[2]))) * 0.125f;
     auto dev = [&](float mw) { return (mw - mean) * (mw - mean); };
@@ -1332,7 +1341,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
                      32.0f * (((dev(q0[0]) + dev(q0[2])) + (dev(q1[0]) + dev(q1[2]))) +
                               ((dev(q2[0]) + dev(q2[2])) + (dev(q3[0]) + dev(q3[2]))));
     const float rstd = rsqrtf(M2 * (1.0f / (BN - 1)) + 1e-5f);
-    const int t = t0 + i * 32 + (lane & 31);
+    const int t = t0 + i * 32 + (ln & 31);
     uint32_t pk[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1349,7 +1358,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
         pk[2 * p][d] = sw[0];
         pk[2 * p + 1][d] = sw[1];
       }
-      const int col = w * 32 + 8 * (2 * p + (lane >> 5));
+      const int col = w * 32 + 8 * (2 * p + (ln >> 5));
       const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
       buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
     }
