@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   stamp();
 
   // unit u (slot u % 3 = SL, a compile-time constant so every LDS offset is an immediate)
-  auto unit = [&](const int u, auto slc, chunk16* wf, chunk16* wn1, const bool last1) {
+  auto unit = [&](const int u, auto slc, chunk16* wf, chunk16* wn1, const bool last1, const bool nosl) {
     constexpr int SL = decltype(slc)::value;
     // B_u: own slice u+1 stores retired; W1 of unit u (issued one unit ago) landed
     __builtin_amdgcn_sched_barrier(0);
@@ -1255,15 +1255,15 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     const int v = u + 2;
     chunk16 c0, sv;
     f32x4 bt, z;
-    read_c0(v, c0, bt);
+    if (!nosl) read_c0(v, c0, bt);
 #pragma unroll
     for (int n = 0; n < 32; ++n) {
       __builtin_amdgcn_sched_barrier(0);
       // slice v: tile x operands at MFMA 7x, conv0 MFMA at 7x+2, store at 7x+4 (tile 16: 28 / 30 / 31)
-      if (n % 7 == 0 && n / 7 < 4) sv = read_sv(v, n / 7);
-      if (n % 7 == 2 && n / 7 < 4) z = mfma_chunk<bf16>(c0, sv, bt);
-      if (n % 7 == 4 && n / 7 < 4) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, n / 7, z);
-      if (p16) {
+      if (!nosl && n % 7 == 0 && n / 7 < 4) sv = read_sv(v, n / 7);
+      if (!nosl && n % 7 == 2 && n / 7 < 4) z = mfma_chunk<bf16>(c0, sv, bt);
+      if (!nosl && n % 7 == 4 && n / 7 < 4) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, n / 7, z);
+      if (!nosl && p16) {
         if (n == 28) sv = read_sv(v, 4);
         if (n == 30) z = mfma_chunk<bf16>(c0, sv, bt);
         if (n == 31) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, 4, z);
@@ -1278,15 +1278,16 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   for (int u = 0; u < 30; u += 6) {
-    unit(u, I0{}, W[0], W[1], false);
-    unit(u + 1, I1{}, W[1], W[0], false);
-    unit(u + 2, I2{}, W[0], W[1], false);
-    unit(u + 3, I0{}, W[1], W[0], false);
-    unit(u + 4, I1{}, W[0], W[1], false);
-    unit(u + 5, I2{}, W[1], W[0], false);
+    unit(u, I0{}, W[0], W[1], false, false);
+    unit(u + 1, I1{}, W[1], W[0], false, false);
+    unit(u + 2, I2{}, W[0], W[1], false, false);
+    unit(u + 3, I0{}, W[1], W[0], false, false);
+    unit(u + 4, I1{}, W[0], W[1], false, false);
+    unit(u + 5, I2{}, W[1], W[0], false, false);
   }
-  unit(30, I0{}, W[0], W[1], false);
-  unit(31, I1{}, W[1], W[0], true);
+  // units 30 and 31 have no slice to make (slices 32, 33 do not exist)
+  unit(30, I0{}, W[0], W[1], false, true);
+  unit(31, I1{}, W[1], W[0], true, true);
 
   // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
   // lane holds C[m = i*32 + lane%32][n = 32w + 8(e/4) + 4(lane/32) + e%4], e = 0..15 (+ b1).
