@@ -1314,13 +1314,12 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     __builtin_amdgcn_sched_barrier(0);
     const f32x4 t = (val(i, 0) + val(i, 1)) + (val(i, 2) + val(i, 3));
     const float mw = xsum((t[0] + t[1]) + (t[2] + t[3])) * (1.0f / 32);
-    f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
+    // M2 of the wave's 32 channels as sum(x^2) - 32 mw^2: packed FMAs on the raw values (x - mw was
+    // 16 scalar FMAs); in fp32 the cancellation is far below the bf16 output rounding
+    f32x4 sq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 d = val(i, q) - mw;
-      d2 += d * d;
-    }
-    const float m2 = xsum((d2[0] + d2[1]) + (d2[2] + d2[3]));
+    for (int q = 0; q < 4; ++q) sq += val(i, q) * val(i, q);
+    const float m2 = fmaxf(xsum((sq[0] + sq[1]) + (sq[2] + sq[3])) - 32.0f * mw * mw, 0.f);
     const int ln = c1_lane();
     if (ln < 32) red2[(i * 32 + ln) * 8 + w] = float2{mw, m2};
   }
@@ -1341,13 +1340,15 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     const float M2 = (((q0[1] + q0[3]) + (q1[1] + q1[3])) + ((q2[1] + q2[3]) + (q3[1] + q3[3]))) +
                      32.0f * (((dev(q0[0]) + dev(q0[2])) + (dev(q1[0]) + dev(q1[2]))) +
                               ((dev(q2[0]) + dev(q2[2])) + (dev(q3[0]) + dev(q3[2]))));
-    const float rstd = rsqrtf(M2 * (1.0f / (BN - 1)) + 1e-5f);
+    float rstd = __builtin_amdgcn_rsqf(M2 * (1.0f / (BN - 1)) + 1e-5f);  // argument >= 1e-5: no denormal path
+    float nmr = -mean * rstd;
+    asm volatile("" : "+v"(rstd), "+v"(nmr));  // y = val * rstd + nmr: one packed FMA per 2 values
     const int t = t0 + i * 32 + (ln & 31);
     uint32_t pk[4][2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4 gg = *(const f32x4*)(EP + 256 + cb + 8 * q), ee = *(const f32x4*)(EP + 512 + cb + 8 * q);
-      const f32x4 v = (val(i, q) - mean) * rstd * gg + ee;
+      const f32x4 v = (val(i, q) * rstd + nmr) * gg + ee;
       pk[q][0] = relu_bf16x2(v[0], v[1]);
       pk[q][1] = relu_bf16x2(v[2], v[3]);
     }
