@@ -334,6 +334,15 @@ __global__ __launch_bounds__(256) void attn2_kernel(AttnArgs a) {
 // 8-byte pieces of one 32-byte column band; XOR-ing the 16-byte chunk with 2*((row>>1)&3) spreads
 // the same-parity rows over the 256-byte bank row (4-way conflicted without it).
 VAP_DEV int vswz3(int row, int c) { return c ^ (((row >> 1) & 3) << 1); }
+// max over the four 16-lane groups (lanes l, l^16, l^32, l^48) by permlane swaps: no LDS round trip
+// and no bpermute address math (inline asm: the builtins given equal operands are miscompiled)
+VAP_DEV float xmax4(float v) {
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  float c = fmaxf(a, b), d = c;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+  return fmaxf(c, d);
+}
 
 __global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
   __shared__ __attribute__((aligned(16))) unsigned char kv[2][2][KB2 * TROW];  // [buf][K,V]
@@ -449,8 +458,7 @@ __global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
           bm = fmaxf(bm, fmaxf(fmaxf(st[qs][kt][0], st[qs][kt][1]), fmaxf(st[qs][kt][2], st[qs][kt][3])));
-        bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+        bm = xmax4(bm);
         if (__ballot(bm > m[qs] + TAU)) {  // wave-uniform: raise the running max, rescale O and l
           const float mn = fmaxf(m[qs], bm);
           const float alpha = __builtin_amdgcn_exp2f(m[qs] - mn);
