@@ -1083,12 +1083,12 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   const int s = blockIdx.y;
   const int t0 = r0 + blockIdx.x * BM2;
   const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
-  unsigned long long stv[8];
+  unsigned long long stv[10];
   int nst = 0;
   auto stamp = [&]() {
     if constexpr (STAMPS) {
       __builtin_amdgcn_sched_barrier(0);
-      if (nst < 8) stv[nst] = __builtin_amdgcn_s_memtime();
+      if (nst < 10) stv[nst] = __builtin_amdgcn_s_memtime();
       ++nst;
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1133,6 +1133,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   chunk16 W[2][4];  // W1 register ring: unit u in set u % 2, loaded one unit ahead
   wload(0, W[0]);
   __syncthreads();
+  stamp();  // waveform segment in LDS
 
   for (int j = tid; j < I_SVN; j += 512) {
     const int r = j / NPOS2, i = j - r * NPOS2;
@@ -1178,6 +1179,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
       vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
     }
   __syncthreads();
+  stamp();  // split-sample rows built
 
   // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; this wave makes channel tile ct
   auto read_c0 = [&](int v, chunk16& c0, f32x4& bt) {
@@ -1369,7 +1371,7 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp();
     if (samp >= 0 && tid == 0)
-      for (int k = 0; k < 8 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
+      for (int k = 0; k < 10 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
   }
 }
 
