@@ -106,10 +106,11 @@ def test_stream_above_cap_recomputes(monkeypatch):
 
 
 def test_heads_per_chunk_equals_once(monkeypatch):
-    """VAP_HEADS_CHUNKED=1 runs the fused heads kernel per back-end time chunk (frame ranges of every
-    clip) instead of once after the last chunk.  The heads are row-wise, so every output is
-    bit-identical to the default schedule.  20 s clips: chunks of 640 and 360 frames."""
+    """By default the fused heads kernel runs per back-end time chunk (frame ranges of every clip);
+    VAP_HEADS_CHUNKED=0 runs it once after the last chunk.  The heads are row-wise, so every output
+    is bit-identical between the two.  20 s clips: chunks of 640 and 360 frames."""
     w = _batch(3, 320000, 900)
+    monkeypatch.setenv("VAP_HEADS_CHUNKED", "0")
     ref = _model().probs(w)
     monkeypatch.setenv("VAP_HEADS_CHUNKED", "1")
     out = _model().probs(w)

@@ -63,8 +63,9 @@ struct vap_handle {
   // measured 3.5 % slower in the back-to-back bench: kept as VAP_TC_FE=0.05,0.12,0.2,0.3,0.42,0.56,0.72)
   std::vector<double> tc_fe{0.1, 0.25, 0.45, 0.7}, tc_be{0.64};
   std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
-  bool heads_chunked = false;  // VAP_HEADS_CHUNKED=1: heads per back-end chunk (shorter tail after the
-                               // recurrence, but small GEMMs: 0.41 vs 0.19 ms; the caller stream binds)
+  bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
+                              // the fused heads kernel takes the first chunk's heads off the tail after
+                              // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
   bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
                              // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
   bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
