@@ -111,7 +111,8 @@ struct LstmSync {
   int time_mode;
   int gx_off = 0;    // gate rows form a ring: step t reads gx row (t + gx_off) mod Tn (streaming)
   unsigned xepoch = 0;  // lstm_pair: launch epoch in the exchange tags (set by launch_lstm_pair)
-  int xplain = 0;       // lstm_pair: exchange stores with the default policy (experiment)
+  int xplain = 0;       // lstm_pair: exchange stores with the default policy even across XCDs (experiment; the
+                        // XCC-id handshake picks that policy by itself when both halves share an XCD)
   int xnowait = 0;      // lstm_pair: do not wait for the partner (timing diagnostics; outputs are garbage)
   int wave_prio = 0;  // lstm_pair (VAP_LSTM_PRIO): waves 0-3 at this s_setprio level, 4-7 at 0 (experiment)
   int handoff_trace = 0;  // lstm_pair (VAP_LSTM_HANDOFF=1): workgroup 0 records s_memrealtime around each hand-off
