@@ -253,6 +253,9 @@ int vap_test_read_lstm_stamps(unsigned long long* out);
  * out[0] launch start, then per time chunk c: out[1+3c] ready wait begins, out[2+3c] ready seen,
  * out[3+3c] done published (49 values) */
 int vap_test_read_lstm_handoff(unsigned long long* out);
+/* XCD handshake of the last pair-LSTM launch, blocks 0..63: own XCC id | partner's << 8 | exchange
+   kept in L2 << 16 | 1 << 24 (written) */
+int vap_test_read_lstm_xcc(unsigned* out);
 
 #ifdef __cplusplus
 }

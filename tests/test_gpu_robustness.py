@@ -116,3 +116,28 @@ def test_heads_per_chunk_equals_once(monkeypatch):
     out = _model().probs(w)
     for k in ref:
         assert torch.equal(out[k], ref[k]), k
+
+
+def test_bf16_repeat_determinism_and_xcd_handshake():
+    """Repeated forwards are bit-identical (the pair recurrence's exchange protocol and the
+    hand-counted vmcnt waits leave no race), and the XCD handshake of the last pair launch keeps
+    the exchange in L2 exactly when both halves of a pair share an XCD."""
+    import ctypes
+    from voiceactivityprojection_amd import _native as N
+
+    m = _model()
+    for n in (37391, 320000):  # the short golden-clip length (T < 128 schedule) and 20 s (time-chunked)
+        w = _batch(2, n, 40)
+        ref = m.probs(w)
+        for _ in range(3):
+            out = m.probs(w)
+            for k in ref:
+                assert torch.equal(out[k], ref[k]), (n, k)
+    m.synchronize()
+    buf = np.zeros(64, dtype=np.uint32)
+    N.check(N.lib().vap_test_read_lstm_xcc(ctypes.c_void_p(buf.ctypes.data)))
+    rec = [int(v) for v in buf if v]
+    assert rec, "no handshake record"
+    for v in rec:
+        own, partner, l2 = v & 255, (v >> 8) & 255, (v >> 16) & 1
+        assert l2 == int(own == partner), (own, partner, l2)

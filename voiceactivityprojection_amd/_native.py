@@ -13,6 +13,7 @@ from typing import Optional
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VAP_LIB_AB=<name> loads _lib/<name> instead (A/B timing of two builds of the engine on one box;
 # the name must be a file in _lib, so the package never loads a library from elsewhere)
+VAP_LIB_AB = os.environ.get("VAP_LIB_AB", "")
 LIB_PATH = os.path.join(_HERE, "_lib", os.path.basename(os.environ.get("VAP_LIB_AB", "")) or "libvap_hip.so")
 
 VAP_OK, VAP_ERR_INVALID, VAP_ERR_TOO_SHORT, VAP_ERR_HIP, VAP_ERR_WEIGHTS, VAP_ERR_UNSUPPORTED = range(6)
@@ -86,6 +87,7 @@ _SIGS = {
     "vap_test_read_lstm_stamps": (ctypes.c_int, [_P]),
     "vap_test_heads": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vap_test_read_lstm_handoff": (ctypes.c_int, [_P]),
+    "vap_test_read_lstm_xcc": (ctypes.c_int, [_P]),
     "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_ffn_packed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
@@ -112,7 +114,9 @@ def lib() -> ctypes.CDLL:
                 "Build it with `make -C voiceactivityprojection_amd/csrc` (hipcc, gfx950).")
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            fn = getattr(l, name)
+            fn = getattr(l, name, None)
+            if fn is None and VAP_LIB_AB:  # an older build under A/B may lack newer test entry points
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = l

@@ -438,6 +438,7 @@ VAP_DEV u32x4 xload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 }
 
 __device__ unsigned long long g_lstm_handoff[1 + 3 * 16];
+__device__ unsigned g_lstm_xcc[64];  // block b < 64 of the last launch: own XCC | partner's << 8 | L2 exchange << 16 | 1 << 24
 
 template <bool PRE, bool ST>
 __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restrict__ gx, int S, int Tn,
@@ -558,8 +559,8 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   // XCC id in its own parity-1 slot with the tag tag_base - 1 (no step uses it; the slot is first
   // overwritten at step 1, after the partner consumed step 0, i.e. after it read this granule) and
   // reads the partner lane's; a timed-out handshake keeps write-through and sets the error word.
-  bool xl2 = sync.xplain != 0;
-  if (!sync.xnowait) {
+  bool xl2 = sync.xplain > 0;  // VAP_LSTM_XPLAIN: 1 plain stores always, -1 never, 0 (default) by handshake
+  if (sync.xplain == 0 && !sync.xnowait) {
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
     const uint32_t htag = tag_base - 1u;
@@ -580,7 +581,9 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    xl2 = xl2 || (ok && __all(pv[0] == xcc && pv[2] == xcc));
+    xl2 = ok && __all(pv[0] == xcc && pv[2] == xcc);
+    if (tid == 0 && b < 64) g_lstm_xcc[b] = xcc | (pv[0] << 8) | ((uint32_t)xl2 << 16) | (1u << 24);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the step loop's hand-counted waits start from zero
   }
   auto run = [&](auto half) {
   constexpr int kown = 4 * decltype(half)::value, krem = 4 - kown;
@@ -860,6 +863,9 @@ template hipError_t launch_lstm<bf16>(const float*, int, int, const bf16*, bf16*
 template hipError_t launch_pack_whh<float>(const float*, float*, hipStream_t);
 template hipError_t launch_pack_whh<bf16>(const float*, bf16*, hipStream_t);
 
+hipError_t read_lstm_xcc(unsigned* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_xcc), sizeof(g_lstm_xcc), 0, hipMemcpyDeviceToHost);
+}
 hipError_t read_lstm_handoff(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstm_handoff), sizeof(g_lstm_handoff), 0, hipMemcpyDeviceToHost);
 }

@@ -120,6 +120,7 @@ struct LstmSync {
 // diagnostics: [0] launch start, then per time chunk c: [1 + 3c] ready wait begins, [2 + 3c] ready seen,
 // [3 + 3c] done published (s_memrealtime, 100 MHz) of the last lstm_pair launch with handoff_trace
 hipError_t read_lstm_handoff(unsigned long long* out);
+hipError_t read_lstm_xcc(unsigned* out);  // XCD handshake record of the last pair launch (64 blocks)
 // prescaled: W_ih / W_hh / biases packed with the gate scales (launch_pack_wih_prescaled,
 // launch_pack_whh_resident(.., true)): gates arrive as -log2e (i, f, o) / 2 log2e (g) multiples
 hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_packed, bf16* out,

@@ -275,5 +275,6 @@ int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_st
 int vap_test_read_gemm_stamps(unsigned long long* out) { return rc_of(read_gemm2_stamps(out)); }
 int vap_test_read_lstm_stamps(unsigned long long* out) { return rc_of(read_lstm_stamps(out)); }
 int vap_test_read_lstm_handoff(unsigned long long* out) { return rc_of(read_lstm_handoff(out)); }
+int vap_test_read_lstm_xcc(unsigned* out) { return rc_of(read_lstm_xcc(out)); }
 
 }  // extern "C"
