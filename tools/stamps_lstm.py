@@ -53,6 +53,12 @@ def main():
     m.probs(w)
     torch.cuda.synchronize()
     show(N, "forward B=4 x 10 s")
+    from voiceactivityprojection_amd.weights import synthetic_batch
+    wb = torch.from_numpy(synthetic_batch(0, 64, 320000)).to(dev)  # the bench workload
+    for _ in range(2):
+        m.probs(wb)
+    torch.cuda.synchronize()
+    show(N, f"bench forward B=64 x 20 s (steps from {os.environ.get('VAP_LSTM_STAMP_T0', '100')})")
 
 
 if __name__ == "__main__":

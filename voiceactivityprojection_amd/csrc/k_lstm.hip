@@ -521,7 +521,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     if constexpr (ST) {
       __builtin_amdgcn_sched_barrier(0);
       const unsigned long long v = __builtin_amdgcn_s_memtime();
-      if (samp && t >= 100 && t < 104) stl[(t - 100) * 5 + k] = v;
+      if (samp && t >= sync.stamp_t0 && t < sync.stamp_t0 + 4) stl[(t - sync.stamp_t0) * 5 + k] = v;
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -700,7 +700,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   if (p == 0) run(std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 1>{});
   if constexpr (ST) {
-    if (samp && Tn >= 104)
+    if (samp && Tn >= sync.stamp_t0 + 4)
       for (int i = 0; i < 20; ++i) g_lstm_stamps[blockIdx.x][i / 5][i % 5] = stl[i];
   }
   if (sync.ready && !sync.time_mode) {
@@ -833,6 +833,8 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
   sy.handoff_trace = hot;
   static const int wprio = getenv("VAP_LSTM_PRIO") ? atoi(getenv("VAP_LSTM_PRIO")) : 0;
   sy.wave_prio = wprio;
+  static const int st0 = getenv("VAP_LSTM_STAMP_T0") ? atoi(getenv("VAP_LSTM_STAMP_T0")) : 100;
+  sy.stamp_t0 = st0;
   const int groups = (S + NS - 1) / NS;
   const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
   static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
