@@ -602,7 +602,8 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     const uint32_t xo_rem = x_rem + (uint32_t)(((t - 1) & 1) * 512 * 16);
     u32x4 xv = {0u, 0u, 0u, 0u};
     if (t > 0) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(xv) : "v"(xo_rem), "s"(xr) : "memory");
-    gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
+    gload(gc, sync.xnostore > 1 ? 0 : t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
+    // (xnostore 2: diagnostics, every step reloads row 0)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const chunk16 hf = hfrag(kown + q);
@@ -651,8 +652,9 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
       asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 2" ::"v"(xo), "v"(xoff), "s"(xr) : "memory");
     // (the s_nops: a VALU write of a store's data VGPRs right after a dwordx3/x4 store is a hazard the
     // compiler does not see through inline asm)
-    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
-                 "s"(orsc) : "memory");
+    if (!sync.xnostore)  // (xnostore: timing diagnostics only, the outputs are garbage)
+      asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
+                   "s"(orsc) : "memory");
     hput(u0, hp);  // own units of h_t (the own-unit reads of this step retired before B1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // B2: own h_t visible to every wave
@@ -833,6 +835,8 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
   sy.handoff_trace = hot;
   static const int wprio = getenv("VAP_LSTM_PRIO") ? atoi(getenv("VAP_LSTM_PRIO")) : 0;
   sy.wave_prio = wprio;
+  static const int xnostore = getenv("VAP_LSTM_XNOSTORE") ? atoi(getenv("VAP_LSTM_XNOSTORE")) : 0;  // diagnostics
+  sy.xnostore = xnostore;
   static const int st0 = getenv("VAP_LSTM_STAMP_T0") ? atoi(getenv("VAP_LSTM_STAMP_T0")) : 100;
   sy.stamp_t0 = st0;
   const int groups = (S + NS - 1) / NS;
