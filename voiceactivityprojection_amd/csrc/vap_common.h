@@ -56,16 +56,31 @@ template <typename T> struct ChunkElems { static constexpr int v = 16 / sizeof(T
 VAP_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 VAP_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-// wave64 butterfly sums over lane bits [lo, hi)
+// wave64 reductions without the LDS crossbar: DPP within rows of 16 (quad swaps, then half-row and
+// row mirrors, each pairing two partial results of equal extent), then v_permlane16/32_swap across
+// rows (inline asm: the builtins given equal operands are miscompiled).  Every pair is combined in
+// both orders, so all 64 lanes end with the bit-identical result.
+template <int CTRL>
+VAP_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <typename Op>
+VAP_DEV float wave_reduce(float v, Op op) {
+  v = op(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+  v = op(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+  v = op(v, dpp_f<0x141>(v));  // row_half_mirror: the other quad of the 8
+  v = op(v, dpp_f<0x140>(v));  // row_mirror: the other 8 of the row
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  float c = op(a, b), d = c;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+  return op(c, d);
+}
 VAP_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float x, float y) { return x + y; });
 }
 VAP_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
 // store 4 consecutive values as T
