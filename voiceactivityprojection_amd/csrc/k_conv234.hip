@@ -304,14 +304,12 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
       float sum = (t[0] + t[1]) + (t[2] + t[3]);
       sum = ck_xsum(sum);
       const float mw = sum * (1.0f / 32);
-      f32x4 d2 = {0.f, 0.f, 0.f, 0.f};
+      // M2 of the wave's 32 channels as sum(x^2) - 32 mw^2 on packed FMAs (x - mw was 16 scalar FMAs)
+      f32x4 sq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 d = val(i, q) - mw;
-        d2 += d * d;
-      }
-      float m2 = (d2[0] + d2[1]) + (d2[2] + d2[3]);
-      m2 = ck_xsum(m2);
+      for (int q = 0; q < 4; ++q) sq += val(i, q) * val(i, q);
+      float m2 = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+      m2 = fmaxf(ck_xsum(m2) - 32.0f * mw * mw, 0.f);
       const int ln = ck_lane();
       if (ln < 32) red[(i * 32 + ln) * 8 + w] = float2{mw, m2};
     }
@@ -333,7 +331,9 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
       const float M2 = (((r0[1] + r0[3]) + (r1[1] + r1[3])) + ((r2[1] + r2[3]) + (r3[1] + r3[3]))) +
                        32.0f * (((dev(r0[0]) + dev(r0[2])) + (dev(r1[0]) + dev(r1[2]))) +
                                 ((dev(r2[0]) + dev(r2[2])) + (dev(r3[0]) + dev(r3[2]))));
-      const float rstd = rsqrtf(M2 * (1.0f / 255) + 1e-5f);
+      float rstd = __builtin_amdgcn_rsqf(M2 * (1.0f / 255) + 1e-5f);  // argument >= 1e-5: no denormal path
+      float nmr = -m * rstd;
+      asm volatile("" : "+v"(rstd), "+v"(nmr));  // y = val * rstd + nmr: packed FMAs
       const int t = t0 + i * 32 + (ln & 31);
       uint32_t pk[4][2];
       // gamma / beta re-read from LDS per row tile (hoisted out of the loop they would hold 32 VGPRs
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
       for (int q = 0; q < 4; ++q) {
         const f32x4 gg = *(const f32x4*)((const unsigned char*)PR + 1024 + pro + 32 * q);
         const f32x4 ee = *(const f32x4*)((const unsigned char*)PR + 2048 + pro + 32 * q);
-        const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) - m) * rstd * gg + ee;
+        const f32x4 v = (DBG & 1) ? val(i, q) : (val(i, q) * rstd + nmr) * gg + ee;
         if constexpr ((DBG & 1) != 0) {
           pk[q][0] = pack_bf16x4(v[0], v[1], v[2], v[3])[0];
           pk[q][1] = pack_bf16x4(v[0], v[1], v[2], v[3])[1];
