@@ -222,22 +222,25 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   }
 
   // ---------------------------------------------------------------- weight stream
-  const bf16* __restrict__ Wo = (const bf16*)g.Wo;
-  const bf16* __restrict__ W1 = (const bf16*)g.W1;
-  const bf16* __restrict__ W2 = (const bf16*)g.W2;
+  // weights through buffer resources: the fragment offset is the lane's 16 bytes plus a scalar part,
+  // no per-load 64-bit address arithmetic on the VALU (the flat form spent ~170 VALU per workgroup)
+  const __amdgpu_buffer_rsrc_t rWo = make_rsrc(g.Wo, 0x7FFFFFF0u), rW1 = make_rsrc(g.W1, 0x7FFFFFF0u),
+                               rW2 = make_rsrc(g.W2, 0x7FFFFFF0u);
+  const uint32_t wlo = (uint32_t)lane * 16u;
   auto wload = [&](int q, chunk16* r) {  // q static after unrolling
-    const bf16* base;
     int kidx;
-    if (OPROJ && q < Q0) {
-      base = Wo;
+    const bool o = OPROJ && q < Q0;
+    bool second = false;
+    if (o) {
       kidx = q;
     } else {
       const int t = q - Q0, s = t >> 4, u = t & 15;
-      base = u < 8 ? W1 : W2;
+      second = u >= 8;
       kidx = s * 8 + (u & 7);
     }
+    const __amdgpu_buffer_rsrc_t rs = o ? rWo : second ? rW2 : rW1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+    for (int i = 0; i < 2; ++i) r[i] = buf_load16(rs, wlo, (uint32_t)((kidx * 16 + 2 * w + i) * 1024));
   };
   chunk16 wr[NPF][2];
 #pragma unroll
@@ -469,22 +472,24 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
     for (int i = 0; i < 2; ++i)
       acc[i][j] = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
 
-  const bf16* __restrict__ Wo = (const bf16*)g.Wo;
-  const bf16* __restrict__ Wp = (const bf16*)g.Wp;
-  const bf16* __restrict__ Wr = (const bf16*)g.Wr;
+  // weights through buffer resources (see block_kernel)
+  const __amdgpu_buffer_rsrc_t rWo = make_rsrc(g.Wo, 0x7FFFFFF0u), rWp = make_rsrc(g.Wp, 0x7FFFFFF0u),
+                               rWr = make_rsrc(g.Wr, 0x7FFFFFF0u);
+  const uint32_t wlo = (uint32_t)lane * 16u;
   auto wload = [&](int q, chunk16* r) {
-    const bf16* base;
     int kidx;
-    if (OPROJ && q < Q0) {
-      base = Wo;
+    const bool o = OPROJ && q < Q0;
+    bool rr = false;
+    if (o) {
       kidx = q;
     } else {
       const int p = (q - Q0) >> 3;
-      base = p < NP ? Wp : Wr;
+      rr = p >= NP;
       kidx = (p < NP ? p : p - NP) * 8 + ((q - Q0) & 7);
     }
+    const __amdgpu_buffer_rsrc_t rs = o ? rWo : rr ? rWr : rWp;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+    for (int i = 0; i < 2; ++i) r[i] = buf_load16(rs, wlo, (uint32_t)((kidx * 16 + 2 * w + i) * 1024));
   };
   chunk16 wr[NPF][2];
 #pragma unroll
@@ -661,11 +666,14 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
   if (tid < 256)
     gbv = *(const f32x4*)((tid < 64 ? g.gamma : tid < 128 ? g.beta : tid < 192 ? g.hbias : g.vw) + (tid & 63) * 4);
 
-  auto wload = [&](int q, chunk16* r) {  // q static after unrolling
-    const bf16* base = q < 8 ? g.Wa : q < 16 ? g.Wb : g.Wh;
+  const __amdgpu_buffer_rsrc_t rWa = make_rsrc(g.Wa, 0x7FFFFFF0u), rWb = make_rsrc(g.Wb, 0x7FFFFFF0u),
+                               rWh = make_rsrc(g.Wh, 0x7FFFFFF0u);
+  const uint32_t wlo = (uint32_t)lane * 16u;
+  auto wload = [&](int q, chunk16* r) {  // q static after unrolling (weights through buffer resources)
+    const __amdgpu_buffer_rsrc_t rs = q < 8 ? rWa : q < 16 ? rWb : rWh;
     const int kidx = q & 7;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) r[i] = *(const chunk16*)(base + (((int64_t)kidx * 16 + 2 * w + i) * 64 + lane) * 8);
+    for (int i = 0; i < 2; ++i) r[i] = buf_load16(rs, wlo, (uint32_t)((kidx * 16 + 2 * w + i) * 1024));
   };
   chunk16 wr[NPF][2];
 #pragma unroll
