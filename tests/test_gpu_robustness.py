@@ -141,3 +141,16 @@ def test_bf16_repeat_determinism_and_xcd_handshake():
     for v in rec:
         own, partner, l2 = v & 255, (v >> 8) & 255, (v >> 16) & 1
         assert l2 == int(own == partner), (own, partner, l2)
+
+
+def test_exchange_policy_does_not_change_outputs(monkeypatch):
+    """The pair recurrence's h exchange policy (XCD-local L2 by handshake, forced write-through with
+    VAP_LSTM_XPLAIN=-1) changes where the bytes travel, not the arithmetic: outputs bit-identical."""
+    m = _model()
+    w = _batch(3, 160000, 77)
+    ref = m.probs(w)
+    monkeypatch.setenv("VAP_LSTM_XPLAIN", "-1")
+    out = m.probs(w)
+    m.synchronize()
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k

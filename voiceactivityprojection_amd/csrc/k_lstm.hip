@@ -827,7 +827,8 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
     sy = *sync;
   }
   sy.xepoch = xepoch;
-  static const int xplain = getenv("VAP_LSTM_XPLAIN") ? atoi(getenv("VAP_LSTM_XPLAIN")) : 0;
+  const char* xpe = getenv("VAP_LSTM_XPLAIN");  // read per launch (tests switch it)
+  const int xplain = xpe ? atoi(xpe) : 0;
   sy.xplain = xplain;
   static const int xnowait = getenv("VAP_LSTM_XNOWAIT") ? atoi(getenv("VAP_LSTM_XNOWAIT")) : 0;  // timing diagnostics only
   sy.xnowait = xnowait;
