@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ lo
 #pragma unroll
   for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
   const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
-  const f32x4 p = e / sum;
+  const f32x4 p = e * (1.0f / sum);  // one IEEE division per lane (four were VALU-bound)
   *(f32x4*)(probs + f * 256 + lane * 4) = p;
   float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
   const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void probs_loss_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
   const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
-  const f32x4 p = e / sum;
+  const f32x4 p = e * (1.0f / sum);  // one IEEE division per lane (four were VALU-bound)
   *(f32x4*)(probs + f * 256 + lane * 4) = p;
   float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
   const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
