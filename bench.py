@@ -3,10 +3,15 @@
 
 Workload (BASELINE.json configs[1]): batch 64 x 20 s stereo @ 16 kHz per GPU, 50 Hz frames, bf16
 perf mode (fp32 accumulate).  One "step" = model.probs(waveform) over the rank's batch, inputs
-already resident in HBM.  With --gpus N > 1 (torchrun, one process per GPU, RCCL) every rank
-processes its own 64 clips (clip seeds = global clip index: data-parallel shards, weak scaling)
-and the compact per-frame outputs (p_now, p_future, vad, H) are gathered to rank 0 with one RCCL
-gather per step (north_star: "single RCCL gather over xGMI for the output probabilities").
+already resident in HBM.
+
+Multi-GPU (BASELINE configs[2]): ``--gpus N`` runs one process per GPU.  Under
+torchrun (WORLD_SIZE set) this process is one rank; without it, ``--gpus N > 1`` starts torchrun
+with N ranks as a child process before anything touches the GPU and exits with its code.  Every
+rank processes its own 64 clips (clip seeds = global clip index: data-parallel shards, weak
+scaling) and writes its outputs into one packed buffer (distributed.PackedOutputs: probs, vad,
+p_now, p_future, H, loss); each step ships that buffer to rank 0 with ONE RCCL gather, issued
+asynchronously so it overlaps the next step's compute (double-buffered).
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline` (dominant kernel,
 HIP-event timed inside the timed region) and `cpu_baseline` (the CPU oracle on a bounded sample).
@@ -14,9 +19,11 @@ HIP-event timed inside the timed region) and `cpu_baseline` (the CPU oracle on a
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +40,7 @@ CLASSES = ["conv0", "conv1", "conv234", "lstm_proj", "lstm_rec", "downsample", "
 
 def class_flops(B: int, n: int, heads: int = 4, channel_layers: int = 1, cross_layers: int = 3, lstm_layers: int = 1):
     """Algorithmic FLOPs per step for each kernel class (2 per MAC; causal attention counts j <= i)."""
-    from voiceactivityprojection_amd._native import frame_lengths
+    from voiceactivityprojection_amd.utils import frame_lengths
 
     L = frame_lengths(n)
     S, T, D = 2 * B, L[5], 256
@@ -77,7 +84,7 @@ def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int =
                       f"{threads} host threads ({el:.1f} s)"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -86,138 +93,245 @@ def main():
     ap.add_argument("--seconds", type=float, default=20.0)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather-probs", action="store_true", help="also gather the 256-way probs to rank 0")
-    args = ap.parse_args()
+    ap.add_argument("--gather", default="all", choices=["all", "compact"],
+                    help="outputs shipped to rank 0: all six probs() outputs, or p_now/p_future/vad/H")
+    # CPU rehearsal of the launcher / gather path (tests/test_bench_launcher.py): gloo ranks on the host
+    # with a stub step that writes rank-tagged outputs; no GPU, no engine
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    """--gpus N > 1 without a torchrun environment: start torchrun with N ranks (one process per GPU)
+    running this script, as a CHILD process (this process has not touched the GPU), and return its
+    exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class _StubModel:
+    """--stub: writes rank-tagged outputs (value = global clip index + key offset) so rank 0 can
+    verify the gathered layout exactly."""
+
+    def __init__(self, first_clip: int):
+        self.first_clip = first_clip
+
+    def probs(self, wav, out):
+        for j, (k, v) in enumerate(out.items()):
+            idx = torch.arange(v.shape[0], dtype=torch.float32).view(-1, *([1] * (v.dim() - 1)))
+            v.copy_((self.first_clip + idx + 1000.0 * j).expand_as(v))
+        return out
+
+    def synchronize(self):
+        pass
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args, argv)
+    return run_rank(args)
+
+
+def run_rank(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
     dist = world > 1
-    if dist:
-        import torch.distributed as tdist
+    import torch.distributed as tdist
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    from voiceactivityprojection_amd.distributed import PackedOutputs, gather_packed
+    from voiceactivityprojection_amd.utils import frame_lengths
 
-    from vap.model import VapGPT
-    from voiceactivityprojection_amd import _native as N
-    from voiceactivityprojection_amd.weights import synthetic_batch, synthetic_state_dict
-
-    sd_np = synthetic_state_dict(seed=0)
-    model = VapGPT(precision=args.precision)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
-    model = model.to(dev).eval()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.stub:
+        dev = torch.device("cpu")
+        if dist:
+            tdist.init_process_group("gloo")
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if dist:
+            tdist.init_process_group("nccl", device_id=dev)
 
     B, n = args.batch, int(args.seconds * 16000)
-    wav = torch.from_numpy(synthetic_batch(rank * B, B, n)).to(dev)
+    T = frame_lengths(n)[5]
+    keys = ("probs", "vad", "p_now", "p_future", "H", "loss") if args.gather == "all" else ("p_now", "p_future", "vad", "H")
+    if args.stub:
+        model, wav, sd_np = _StubModel(rank * B), None, None
+    else:
+        from vap.model import VapGPT
+        from voiceactivityprojection_amd.weights import synthetic_batch, synthetic_state_dict
+
+        sd_np = synthetic_state_dict(seed=0)
+        model = VapGPT(precision=args.precision)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+        model = model.to(dev).eval()
+        wav = torch.from_numpy(synthetic_batch(rank * B, B, n)).to(dev)
+
+    # double-buffered packed outputs: step i writes packs[i % 2] while the gather of step i - 1 runs
+    packs = [PackedOutputs(B, T, dev, keys) for _ in range(2)]
+    recvs = [[torch.empty_like(p.flat) for _ in range(world)] if dist and rank == 0 else None for p in packs]
+    works = [None, None]
+    state = {"i": 0}
+
+    def step():
+        j = state["i"] % 2
+        state["i"] += 1
+        if works[j] is not None:
+            works[j].wait()  # the gather that last read this buffer (stream-ordered on RCCL)
+        model.probs(wav, out=packs[j].views())
+        if dist:
+            works[j], _ = gather_packed(packs[j], dst=0, recv=recvs[j], async_op=True)
+
+    def drain():
+        for j in range(2):
+            if works[j] is not None:
+                works[j].wait()
+                works[j] = None
+
+    def device_sync():
+        if not args.stub:
+            torch.cuda.synchronize(dev)
+
+    for _ in range(max(1, args.warmup)):  # warm-up (includes weight packing)
+        step()
+    drain()
+    device_sync()
+    model.synchronize()
+
+    breakdown, dominant, lib, h, N = {}, None, None, None, None
     flops, L = class_flops(B, n)
     if args.precision == "bf16":  # conv0 is fused into the conv1 kernel (k_conv01.hip)
         flops["conv1"] += flops["conv0"]
         flops["conv0"] = 0.0
-    T = L[5]
+    if not args.stub:
+        # per-class breakdown (one extra untimed forward per class) to find the dominant kernel
+        from voiceactivityprojection_amd import _native as N
 
-    def step():
-        out = model.probs(wav)
-        if dist:
-            keys = ["p_now", "p_future", "vad", "H"] + (["probs"] if args.gather_probs else [])
-            for k in keys:
-                t = out[k].contiguous()
-                bufs = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-                tdist.gather(t, bufs, dst=0)
-        return out
+        h = model._native(dev)
+        lib = N.lib()
+        for cls in CLASSES:
+            N.check(lib.vap_timing(h, N.KERNEL_CLASS[cls]))
+            model.probs(wav, out=packs[0].views())
+            tot, cnt = ctypes.c_double(), ctypes.c_int()
+            N.check(lib.vap_timing_read(h, ctypes.byref(tot), ctypes.byref(cnt)))
+            breakdown[cls] = round(tot.value, 4)
+        N.check(lib.vap_timing(h, 0))
+        model.synchronize()
+        # the roofline is reported for the dominant kernel ON THE CRITICAL PATH (the caller's stream):
+        # the LSTM recurrence runs as one persistent launch on a side stream, overlapped with (and
+        # gated by) the front / back ends, so its launch time is mostly waiting, not work
+        # (single-kernel classes only: tr_gemm / heads mix several kernels)
+        dominant = max(("conv1", "conv234", "lstm_proj", "downsample", "attn"), key=breakdown.get)
+        N.check(lib.vap_timing(h, N.KERNEL_CLASS[dominant]))
 
-    # warm-up (includes weight packing)
-    for _ in range(max(1, args.warmup)):
-        step()
-    torch.cuda.synchronize(dev)
-
-    # per-class breakdown (one extra untimed step per class) to find the dominant kernel
-    h = model._native(dev)
-    lib = N.lib()
-    breakdown = {}
-    for cls in CLASSES:
-        N.check(lib.vap_timing(h, N.KERNEL_CLASS[cls]))
-        model.probs(wav)
-        tot, cnt = __import__("ctypes").c_double(), __import__("ctypes").c_int()
-        N.check(lib.vap_timing_read(h, __import__("ctypes").byref(tot), __import__("ctypes").byref(cnt)))
-        breakdown[cls] = round(tot.value, 4)
-    N.check(lib.vap_timing(h, 0))
-    # the roofline is reported for the dominant kernel ON THE CRITICAL PATH (the caller's stream):
-    # the LSTM recurrence runs as one persistent launch on a side stream, overlapped with (and
-    # gated by) the front / back ends, so its launch time is mostly waiting, not work
-    # (single-kernel classes only: tr_gemm / heads mix several kernels)
-    dominant = max(("conv1", "conv234", "lstm_proj", "downsample", "attn"), key=breakdown.get)
-
-    # timed region: K steps, HIP events around every launch of the dominant kernel class
-    N.check(lib.vap_timing(h, N.KERNEL_CLASS[dominant]))
+    # timed region: K steps (+ their gathers), HIP events around every launch of the dominant class
     if dist:
         tdist.barrier()
-    torch.cuda.synchronize(dev)
+    device_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    drain()
+    device_sync()
+    model.synchronize()  # a timed-out recurrence hand-off fails the bench instead of reporting a number
     if dist:
         tdist.barrier()
     el = time.perf_counter() - t0
-    import ctypes
 
     tot, cnt = ctypes.c_double(), ctypes.c_int()
-    N.check(lib.vap_timing_read(h, ctypes.byref(tot), ctypes.byref(cnt)))
-    N.check(lib.vap_timing(h, 0))
+    if not args.stub:
+        N.check(lib.vap_timing_read(h, ctypes.byref(tot), ctypes.byref(cnt)))
+        N.check(lib.vap_timing(h, 0))
     if dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         el = float(t.item())
 
+    gather_info = None
+    if dist:
+        last = (state["i"] - 1) % 2
+        verified = None
+        if rank == 0:
+            got = recvs[last]
+            verified = bool(torch.equal(got[0], packs[last].flat))  # rank 0's own shard, bit for bit
+            if args.stub:  # every rank's region holds exactly its clips' tags
+                for r in range(world):
+                    exp = _StubModel(r * B).probs(None, PackedOutputs(B, T, "cpu", keys).views())
+                    view = packs[last].views(B, flat=got[r])
+                    verified = verified and all(torch.equal(view[k], exp[k]) for k in keys)
+            else:
+                verified = verified and all(bool(torch.isfinite(g).all()) for g in got)
+        gather_info = {"collective": "torch.distributed.gather" + (" (gloo)" if args.stub else " (RCCL)"),
+                       "calls_per_step": 1, "bytes_per_rank": packs[0].flat.numel() * 4, "keys": list(keys),
+                       "overlapped_with_next_step": True, "verified": verified}
+
     if rank == 0:
         audio_s = world * B * args.seconds * args.steps
         value = audio_s / el
-        dom_ms_per_launch = tot.value / max(1, cnt.value)
-        launches_per_step = max(1, cnt.value // args.steps)
-        flop_per_launch = flops[dominant] / launches_per_step
-        achieved = flop_per_launch / (dom_ms_per_launch * 1e-3) / 1e12
-        peak = PEAK_TFLOPS[args.precision]
-        # HBM traffic of the dominant kernel: PMC-measured bytes per output row (profiles/, collected
-        # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
-        # by the concurrent LSTM) x the rows of one launch here
-        traffic, traffic_src = None, None
-        tp = os.path.join(REPO, "profiles", "r2_traffic_pmc.json")  # the current conv01 kernel (v11)
-        if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
-            per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
-            rows_per_launch = 2 * B * L[1] / launches_per_step
-            traffic = round(per_row * rows_per_launch / 1e9, 3)
-            traffic_src = "profiles/r2_traffic_pmc.json (GB per launch)"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "audio-s/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": f"batch={B} x {args.seconds:g}s stereo @16kHz per GPU, 50Hz frames (T={T}), "
-                                   f"{args.precision} (BASELINE.json configs[1])",
+                                   f"{args.precision} (BASELINE.json configs[{1 if world == 1 else 2}])",
                        "global_batch": world * B, "seconds_per_clip": args.seconds, "frames": T,
                        "parallelism": f"dp{world}", "step": "VapGPT.probs (forward + probs epilogue + labels/loss)"
-                                                            + (" + RCCL gather to rank 0" if dist else "")},
-            "roofline": {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "flop_per_launch": flop_per_launch, "ms_per_launch": round(dom_ms_per_launch, 4),
-                         "launches": cnt.value},
-            "breakdown_ms_per_step": breakdown,
-            "breakdown_note": "ms of each kernel class per step (HIP events on its stream); lstm_rec is one persistent "
-                              "side-stream launch overlapped with the caller-stream classes (its time includes "
-                              "waiting for the time chunks), the other classes run back to back on the caller's stream",
-            "model_tflops_per_s": round(sum(flops.values()) * args.steps * world / el / 1e12, 2),
+                                                            + (" + one RCCL gather to rank 0" if dist else "")},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if gather_info is not None:
+            line["gather"] = gather_info
+        if not args.stub:
+            dom_ms_per_launch = tot.value / max(1, cnt.value)
+            launches_per_step = max(1, cnt.value // args.steps)
+            flop_per_launch = flops[dominant] / launches_per_step
+            achieved = flop_per_launch / (dom_ms_per_launch * 1e-3) / 1e12
+            peak = PEAK_TFLOPS[args.precision]
+            # HBM traffic of the dominant kernel: PMC-measured bytes per output row (profiles/, collected
+            # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
+            # by the concurrent LSTM) x the rows of one launch here
+            traffic, traffic_src = None, None
+            tp = os.path.join(REPO, "profiles", "r2_traffic_pmc.json")  # the current conv01 kernel (v11)
+            if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
+                per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
+                rows_per_launch = 2 * B * L[1] / launches_per_step
+                traffic = round(per_row * rows_per_launch / 1e9, 3)
+                traffic_src = "profiles/r2_traffic_pmc.json (GB per launch)"
+            line["roofline"] = {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                                "traffic_source": traffic_src, "flop_per_launch": flop_per_launch,
+                                "ms_per_launch": round(dom_ms_per_launch, 4), "launches": cnt.value}
+            line["breakdown_ms_per_step"] = breakdown
+            line["breakdown_note"] = ("ms of each kernel class per step (HIP events on its stream); lstm_rec is one "
+                                      "persistent side-stream launch overlapped with the caller-stream classes (its "
+                                      "time includes waiting for the time chunks), the other classes run back to "
+                                      "back on the caller's stream")
+            line["model_tflops_per_s"] = round(sum(flops.values()) * args.steps * world / el / 1e12, 2)
+        if world == 1 and not args.no_cpu_baseline and not args.stub:
             line["cpu_baseline"] = cpu_baseline(args.seconds, sd_np)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

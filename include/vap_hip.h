@@ -227,6 +227,9 @@ int vap_test_block_packed(float* x, const void* o, int M, const void* Wop, const
 /* workspace plan of a forward (diagnostics): byte offsets of X1..X4 (conv1..4 rows), GX (gate rows),
  * H0 (LSTM h), X (residual stream), the total, then the per-sequence strides s1..s4, sh (elements) */
 int vap_test_plan(const vap_handle* h, int batch, int64_t n_samples, int64_t* out);
+/* pair-recurrence exchange tag counter of a handle (tests): *get = the last tag issued; set >= 0 moves it (e.g.
+ * next to the 32-bit wrap, which the next launch handles by clearing the exchange slots) */
+int vap_test_xtag(vap_handle* h, int64_t set, int64_t* get);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled fused-block workgroups (VAP_BLOCK_STAMPS=1) */

@@ -63,6 +63,7 @@ def step_extraction(waveform, model, device="cpu", context_time=20, step_time=5,
         o = model.probs(waveform[..., -chunk_samples:].to(device))
         for k in OUT_KEYS:
             out[k] = torch.cat([out[k], o[k][:, -omitted:]], dim=1)
+    model.synchronize()  # raises if a recurrence hand-off timed out (the outputs would be invalid)
     return batch_to_device(out, "cpu")
 
 
@@ -118,7 +119,9 @@ def main(argv=None):
         ctx, step = (args.chunk_time - args.step_time, args.step_time) if args.honor_chunk_args else (20, 5)
         out = step_extraction(waveform, model, device, context_time=ctx, step_time=step)
     else:
-        out = batch_to_device(model.probs(waveform.to(device)), "cpu")
+        out = model.probs(waveform.to(device))
+        model.synchronize()  # raises if a recurrence hand-off timed out (the outputs would be invalid)
+        out = batch_to_device(out, "cpu")
 
     for k, v in out.items():
         if isinstance(v, torch.Tensor):

@@ -88,12 +88,15 @@ class _OracleModel:
         self.sd = sd
         self.calls = 0
 
-    def probs(self, w):
+    def probs(self, w, out=None):
         import vap_oracle as O
 
         self.calls += 1
         assert w.shape[0] > 0, "the engine rejects an empty batch"
-        return O.probs(w, self.sd)
+        res = O.probs(w, self.sd)
+        for k, v in (out or {}).items():
+            v.copy_(res[k])
+        return res
 
 
 def _empty_shard_worker(rank, world, port, out_q):
@@ -143,6 +146,6 @@ def test_empty_shards_join_the_gather():
     assert got[1][1] is None and got[2][1] is None
     sd = O.state_dict_to_torch(synthetic_state_dict(seed=0))
     ref = O.probs(torch.from_numpy(np.stack([synthetic_waveform(500, 36000)])), sd)
-    for k in ("p_now", "p_future", "vad", "H"):
+    for k in ("probs", "p_now", "p_future", "vad", "H", "loss"):
         assert got[0][1][k].shape == tuple(ref[k].shape)
         np.testing.assert_allclose(got[0][1][k], ref[k].numpy(), atol=1e-5, rtol=1e-5)

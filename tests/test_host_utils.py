@@ -23,6 +23,9 @@ class OracleModel:
     def probs(self, w):
         return O.probs(w, self.sd)
 
+    def synchronize(self):
+        self.synced = True
+
 
 def test_step_extraction_matches_per_fold_reference_loop():
     import run
@@ -120,3 +123,25 @@ def test_vad_utils_match_reference_semantics():
     assert f[:, 0].tolist() == [0, 0, 1, 1, 1, 1, 1, 0, 0, 0]
     o = vad_omit_spikes(v.clone(), max_omit_time=0.02, frame_hz=50)
     assert o[:, 0].tolist() == [0, 0, 1, 1, 1, 0, 0, 0, 0, 0]
+
+
+def test_vad_utils_vs_reference_fixture(golden):
+    """The build's VAD helpers against the reference's own (tools/gen_golden.py utils, vap/utils.py):
+    run lengths, fill-silence-then-omit-spike at several limits, onehot -> list -> onehot."""
+    from voiceactivityprojection_amd.utils import (find_island_idx_len, vad_fill_silences, vad_list_to_onehot,
+                                                   vad_omit_spikes, vad_onehot_to_vad_list)
+
+    g = golden("vad_utils")
+    for i in range(4):
+        va = torch.from_numpy(g[f"va_{i}"])
+        idx, dur, val = find_island_idx_len(va[:, 0])
+        np.testing.assert_array_equal(np.stack([idx.numpy(), dur.numpy(), val.numpy().astype(np.int64)]),
+                                      g[f"island_{i}"])
+        for fill, omit in ((0.02, 0.02), (0.06, 0.1), (0.2, 0.04)):
+            v = vad_omit_spikes(vad_fill_silences(va.clone(), max_fill_time=fill, frame_hz=50),
+                                max_omit_time=omit, frame_hz=50)
+            np.testing.assert_array_equal(v.numpy(), g[f"post_{i}_{fill}_{omit}"], err_msg=f"{i} {fill} {omit}")
+        lists = vad_onehot_to_vad_list(va[None], frame_hz=50, ipu_thresh_time=0.1)
+        assert lists == json.loads(str(g[f"list_{i}"])), i
+        np.testing.assert_array_equal(vad_list_to_onehot(lists[0], duration=va.shape[0] / 50, frame_hz=50).numpy(),
+                                      g[f"onehot_{i}"])

@@ -62,6 +62,36 @@ def test_batch_20s(golden):
     np.testing.assert_allclose(out["probs"][:, :8].numpy(), g["probs_head"], atol=TOL)
 
 
+@pytest.mark.slow
+def test_bench4_clip(golden):
+    """The bench configuration's fixture (tools/gen_golden.py bench4): its inputs are the bench's own
+    synthetic_batch, and the oracle reproduces the reference on one of its clips."""
+    from voiceactivityprojection_amd.weights import synthetic_batch
+
+    g = golden("bench4_20s")
+    w = synthetic_batch(0, 4, int(g["n_samples"]))
+    np.testing.assert_allclose([w.astype(np.float64).sum(), (w.astype(np.float64) ** 2).sum()], g["wav_stats"],
+                               rtol=1e-12)
+    out = O.probs(torch.from_numpy(w[2:3]), _sd())
+    _check(out, {k: g[k][2:3] for k in ("vad", "p_now", "p_future", "H", "loss")})
+    np.testing.assert_allclose(out["probs"][:, ::10].numpy(), g["probs_stride10"][2:3], atol=TOL)
+
+
+def test_example_wav_loader_and_oracle(golden):
+    """BASELINE configs[0]: the build's load_waveform on the reference's example wav gives the fixture's
+    input (int16 / 32768, 24 -> 16 kHz, 37392 samples, zero second channel), and the oracle matches
+    the reference's probs on it.  (The resampler itself is unpinned: torchaudio is absent.)"""
+    from voiceactivityprojection_amd.audio import load_waveform
+
+    g = golden("example_wav")
+    x, sr = load_waveform(os.path.join(os.path.dirname(__file__), "golden", "student_long_female_en-US-Wavenet-G.wav"))
+    assert sr == 16000 and tuple(x.shape) == (1, 37392)
+    np.testing.assert_array_equal(x.numpy(), g["waveform"][0, :1])
+    assert not g["waveform"][0, 1].any()
+    out = O.probs(torch.from_numpy(g["waveform"]), _sd())
+    _check(out, g, keys=("probs", "vad", "p_now", "p_future", "H", "loss"))
+
+
 @pytest.mark.parametrize("name", ["len_37392", "len_min"])
 def test_ragged_lengths(golden, name):
     g = golden(name)

@@ -230,12 +230,101 @@ def gen_mono():
     print("wrote mono.npz", out["logits"].shape)
 
 
+def gen_bench4():
+    """(i) The bench configuration's clips (BASELINE configs[1]: 20 s stereo, clip seeds 0..3 of the
+    bench's own synthetic_batch): every per-frame output in full, the 256-way probs on every 10th
+    frame, so the bf16 perf path is pinned to the reference directly (not to the engine's fp32 mode)."""
+    torch.set_num_threads(8)
+    model = build_model(1)
+    from voiceactivityprojection_amd.weights import synthetic_batch
+
+    n = 320000
+    wav = synthetic_batch(0, 4, n)
+    r = run(model, wav)
+    np.savez_compressed(
+        os.path.join(OUT, "bench4_20s.npz"), clip_start=0, n_samples=n, wav_stats=wav_stats(wav),
+        vad=r["vad"], p_now=r["p_now"], p_future=r["p_future"], H=r["H"], loss=r["loss"],
+        probs_stride10=r["probs"][:, ::10], vad_logits=r["vad_logits"])
+    print("wrote bench4_20s.npz", r["probs"].shape)
+
+
+EXAMPLE_WAV = "student_long_female_en-US-Wavenet-G.wav"
+
+
+def gen_example():
+    """(j) BASELINE configs[0] (run.py:190-279 on example/student_long_female_en-US-Wavenet-G.wav): the
+    reference VapGPT.probs on the waveform exactly as the build's run.py feeds it (the build's
+    load_waveform: int16 / 32768, 24 -> 16 kHz sinc resample; mono -> zero second channel,
+    run.py:219-221).  The resampler is the build's restatement of torchaudio's (absent here), so
+    RESAMPLING is unpinned; this fixture pins everything after it.  The wav itself is copied next to
+    the fixture (tests/golden/, a reference data file) because the GPU box has no /root/reference."""
+    import shutil
+
+    torch.set_num_threads(8)
+    from voiceactivityprojection_amd.audio import load_waveform
+
+    src = os.path.join(REF, "example", EXAMPLE_WAV)
+    shutil.copyfile(src, os.path.join(OUT, EXAMPLE_WAV))
+    x, sr = load_waveform(src, sample_rate=16000)
+    if x.shape[0] == 1:
+        x = torch.cat((x, torch.zeros_like(x)))
+    wav = x.unsqueeze(0).numpy()
+    model = build_model(1)
+    r = run(model, wav)
+    np.savez_compressed(os.path.join(OUT, "example_wav.npz"), waveform=wav, sample_rate=sr,
+                        probs=r["probs"], vad=r["vad"], p_now=r["p_now"], p_future=r["p_future"], H=r["H"],
+                        loss=r["loss"])
+    print("wrote example_wav.npz", wav.shape, r["probs"].shape)
+
+
+def gen_utils():
+    """(k) The reference's host VAD utilities (vap/utils.py:21-49, 170-272) on seeded binary VAD: run
+    lengths, silence filling / spike omission at several limits, onehot <-> list conversions.  The
+    build's voiceactivityprojection_amd/utils.py and the native vad_post_kernel are pinned to them."""
+    import_reference(1)
+    from vap import utils as U
+
+    rng = np.random.default_rng(9)
+    cases = {}
+    for i, T in enumerate((1, 7, 60, 333)):
+        runs = rng.integers(1, 9, size=(2, T))
+        va = np.zeros((T, 2), dtype=np.float32)
+        for c in range(2):
+            edges = np.cumsum(runs[c])
+            flips = np.zeros(T, dtype=np.int64)
+            flips[edges[edges < T]] = 1
+            va[:, c] = ((np.cumsum(flips) + c) % 2).astype(np.float32)
+        cases[f"va_{i}"] = va
+        idx, dur, val = U.find_island_idx_len(torch.from_numpy(va[:, 0]))
+        cases[f"island_{i}"] = np.stack([idx.numpy(), dur.numpy(), val.numpy().astype(np.int64)])
+        for fill, omit in ((0.02, 0.02), (0.06, 0.1), (0.2, 0.04)):
+            v = U.vad_fill_silences(torch.from_numpy(va.copy()), max_fill_time=fill, frame_hz=50)
+            v = U.vad_omit_spikes(v, max_omit_time=omit, frame_hz=50)
+            cases[f"post_{i}_{fill}_{omit}"] = v.numpy()
+        lists = U.vad_onehot_to_vad_list(torch.from_numpy(va[None]), frame_hz=50, ipu_thresh_time=0.1)
+        cases[f"list_{i}"] = np.array(json.dumps(lists))
+        back = U.vad_list_to_onehot(lists[0], duration=T / 50, frame_hz=50)
+        cases[f"onehot_{i}"] = back.numpy()
+    np.savez_compressed(os.path.join(OUT, "vad_utils.npz"), **cases)
+    print("wrote vad_utils.npz", len(cases))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "attention":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "attention":
         gen_attention()
-    elif len(sys.argv) > 1 and sys.argv[1] == "mono":
+    elif which == "mono":
         gen_mono()
+    elif which == "bench4":
+        gen_bench4()
+    elif which == "example":
+        gen_example()
+    elif which == "utils":
+        gen_utils()
     else:
         main()
         gen_attention()
         gen_mono()
+        gen_bench4()
+        gen_example()
+        gen_utils()

@@ -67,6 +67,7 @@ _SIGS = {
                                            ctypes.c_int, _P, _P]),
     "vap_synchronize": (ctypes.c_int, [_P, _P]),
     "vap_test_plan": (ctypes.c_int, [_P, ctypes.c_int, _I64, _P]),
+    "vap_test_xtag": (ctypes.c_int, [_P, _I64, ctypes.POINTER(_I64)]),
     "vap_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "vap_timing_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "vap_test_gemm": (ctypes.c_int, [ctypes.c_int, _P, _I64, _I64, _P, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
@@ -115,8 +116,12 @@ def lib() -> ctypes.CDLL:
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(l, name, None)
-            if fn is None and VAP_LIB_AB:  # an older build under A/B may lack newer test entry points
-                continue
+            if fn is None:
+                if VAP_LIB_AB:  # an older build under A/B may lack newer test entry points
+                    continue
+                raise NativeLibraryMissing(
+                    f"{LIB_PATH} does not export {name} (declared in include/vap_hip.h): the library is stale; "
+                    "rebuild it with `make -C voiceactivityprojection_amd/csrc`.")
             fn.restype = res
             fn.argtypes = args
         _lib = l

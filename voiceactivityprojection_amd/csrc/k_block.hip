@@ -700,21 +700,36 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
   }
   if (tid < 256) *(f32x4*)(GB + tid * 4) = gbv;
   __syncthreads();
-  {  // va_classifier (model.py:257-259) of both speakers from the panels: 4 threads per (row, speaker)
+  {  // va_classifier (model.py:257-259) of both speakers: 4 threads per (row, speaker), 64 columns each,
+     // from the fp32 rows of x (g.xf, as the reference) or else the bf16 panels
     const int r = tid >> 3, sp = (tid >> 2) & 1, part = tid & 3;
-    const unsigned char* img = sp ? P : H;
+    const int m = m0 + r;
     float dsum = 0.f;
+    if (g.xf) {
+      if (m < g.M) {
+        const float* xr = g.xf + (int64_t)(m / g.T) * 2 * g.x_seq + (int64_t)(m % g.T) * D + sp * g.x_seq + part * 64;
+        f32x4 v[16];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = part * 8 + k;
-      const bf16x8 v = *(const bf16x8*)(img + r * ROWB + xswz(r, c) * 16);
-      const f32x4 w0 = *(const f32x4*)(GB + 768 + c * 8), w1 = *(const f32x4*)(GB + 768 + c * 8 + 4);
-      dsum += (((float)v[0] * w0[0] + (float)v[1] * w0[1]) + ((float)v[2] * w0[2] + (float)v[3] * w0[3])) +
-              (((float)v[4] * w1[0] + (float)v[5] * w1[1]) + ((float)v[6] * w1[2] + (float)v[7] * w1[3]));
+        for (int k = 0; k < 16; ++k) v[k] = *(const f32x4*)(xr + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const f32x4 wv = *(const f32x4*)(GB + 768 + part * 64 + 4 * k);
+          dsum += (v[k][0] * wv[0] + v[k][1] * wv[1]) + (v[k][2] * wv[2] + v[k][3] * wv[3]);
+        }
+      }
+    } else {
+      const unsigned char* img = sp ? P : H;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = part * 8 + k;
+        const bf16x8 v = *(const bf16x8*)(img + r * ROWB + xswz(r, c) * 16);
+        const f32x4 w0 = *(const f32x4*)(GB + 768 + c * 8), w1 = *(const f32x4*)(GB + 768 + c * 8 + 4);
+        dsum += (((float)v[0] * w0[0] + (float)v[1] * w0[1]) + ((float)v[2] * w0[2] + (float)v[3] * w0[3])) +
+                (((float)v[4] * w1[0] + (float)v[5] * w1[1]) + ((float)v[6] * w1[2] + (float)v[7] * w1[3]));
+      }
     }
     dsum += __shfl_xor(dsum, 1, 64);
     dsum += __shfl_xor(dsum, 2, 64);
-    const int m = m0 + r;
     const int64_t om = g.out_T ? (int64_t)(m / g.T) * g.out_T + g.out_f0 + m % g.T : m;
     if (part == 0 && m < g.M) g.vad[om * 2 + sp] = dsum + g.vb[0];
   }

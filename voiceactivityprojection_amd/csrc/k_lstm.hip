@@ -468,7 +468,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   // exchange slots of this pair: ours [p][parity], the partner's [1-p][parity]; lane tid <-> lane tid
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xbuf + (int64_t)grp * P_SLOT, (uint32_t)(P_SLOT * 16));
   const uint32_t x_own = (uint32_t)(((p * 2) * 512 + tid) * 16), x_rem = (uint32_t)((((1 - p) * 2) * 512 + tid) * 16);
-  const uint32_t tag_base = sync.xepoch * (uint32_t)(Tn + 1) + 1u;  // tag of step t: tag_base + t (never 0)
+  const uint32_t tag_base = sync.xtag + 1u;  // tag of step t: tag_base + t; the handshake's: sync.xtag (never 0)
 
   int ra = 0, rb = -1;
   if (sync.ready) {
@@ -815,8 +815,9 @@ size_t lstm_pair_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * P_SLOT
 int lstm_pair_workgroups(int S) { return 2 * ((S + NS - 1) / NS); }
 
 hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
-                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xepoch) {
-  if (S <= 0 || Tn <= 0 || !xbuf) return hipErrorInvalidValue;
+                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag) {
+  if (S <= 0 || Tn <= 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn > 0xFFFFFFFFull)
+    return hipErrorInvalidValue;
   LstmSync sy{};
   if (sync) {
     if (sync->nr < 1 || sync->nr > 16 || sync->seq_end[sync->nr - 1] < (sync->time_mode ? Tn : S))
@@ -826,7 +827,7 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
     if (sync->gx_off < 0 || sync->gx_off >= Tn) return hipErrorInvalidValue;
     sy = *sync;
   }
-  sy.xepoch = xepoch;
+  sy.xtag = xtag;
   const char* xpe = getenv("VAP_LSTM_XPLAIN");  // read per launch (tests switch it)
   const int xplain = xpe ? atoi(xpe) : 0;
   sy.xplain = xplain;

@@ -103,7 +103,9 @@ struct vap_handle {
   bool convk4 = true;
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
-  unsigned xepoch = 0;
+  // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
+  // slot left by any earlier launch never holds a tag a later launch waits for); wraps by clearing xbuf
+  unsigned xtag = 0;
   int test_drop_ready = -1;  // VAP_TEST_DROP_READY=c (tests only): never publish ready[c] -> the wait times out
   int lstm_max_wg = 0;  // VAP_LSTM_MAX_WG: persistent recurrence launches at most this many workgroups
   unsigned epoch = 0;
@@ -172,7 +174,8 @@ struct vap_handle {
       }
     }
     if (!streams_ready && xbuf) (void)hipFree(xbuf);
-    for (auto& kv : params) (void)hipFree(kv.second.dev);
+    for (auto& kv : params)
+      if (kv.second.dev) (void)hipFree(kv.second.dev);
     for (auto& kv : packed) (void)hipFree(kv.second);
     for (auto& kv : fpacked) (void)hipFree(kv.second);
     for (auto& e : ev) {
@@ -880,6 +883,7 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
                    (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"), h->P("ar.combinator.ln.bias"),
                    h->P("vap_head.bias"), logits + r.c0 * (int64_t)T_ * 256, 1e-5f, h->P("va_classifier.weight"),
                    h->P("va_classifier.bias"), vadl + r.c0 * (int64_t)T_ * 2};
+      ha.xf = X;
       HIPCHK(launch_heads(ha, st));
       return VAP_OK;
     }
@@ -1112,11 +1116,19 @@ int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* ou
     h->xbuf_bytes = 0;
     const size_t bytes = std::max(need, (size_t)64 * slot);
     HIPCHK(hipMalloc(&h->xbuf, bytes));
-    HIPCHK(hipMemset(h->xbuf, 0, bytes));  // tags carry the launch epoch (>= 1): zero never matches
+    HIPCHK(hipMemset(h->xbuf, 0, bytes));  // tags are >= 1: zero never matches
     h->xbuf_bytes = bytes;
   }
+  const uint64_t span = (uint64_t)L4 + 1;
+  if ((uint64_t)h->xtag + span + 1 > 0xFFFFFFFFull) {  // tag space exhausted (~4e9 steps): restart at 1
+    HIPCHK(hipDeviceSynchronize());                    // no launch may still read the old tags
+    HIPCHK(hipMemset(h->xbuf, 0, h->xbuf_bytes));
+    h->xtag = 0;
+  }
+  const unsigned tag0 = h->xtag + 1;  // this launch: tags tag0 .. tag0 + L4
+  h->xtag += (unsigned)span;
   HIPCHK(launch_lstm_pair(GX, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
-                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, ++h->xepoch));
+                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0));
   return VAP_OK;
 }
 
@@ -1271,6 +1283,7 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
                  (const bf16*)h->W<T>("comb_b@rp"), (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"),
                  h->P("ar.combinator.ln.bias"), h->P("vap_head.bias"), logits, 1e-5f, h->P("va_classifier.weight"),
                  h->P("va_classifier.bias"), vadl, T_, f0};
+    ha.xf = X + o;
     HIPCHK(launch_heads(ha, st));
     return VAP_OK;
   }
@@ -1728,8 +1741,8 @@ int stream_main_graph(vap_stream* s, const TcSched& t, const LstmSync& sy, const
   const float* wav = s->win[nxt];
   int rc, published = 0;
   auto publish = [&](int64_t rows_ready) -> int {
-    while (published < t.nch && t.seq_end[published] <= rows_ready)
-      HIPCHK(launch_flag_set((unsigned*)sy.ready + published++, sy.epoch, st));
+    for (; published < t.nch && t.seq_end[published] <= rows_ready; ++published)
+      if (published != h->test_drop_ready) HIPCHK(launch_flag_set((unsigned*)sy.ready + published, sy.epoch, st));
     return VAP_OK;
   };
   if (s->keep0 > 0 && (rc = conv_rows(h, p, wav, W, s->ws, s->gx, 0, s->keep0, st, off))) return rc;
@@ -1833,8 +1846,8 @@ int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad
   if ((rc = tc_launch_lstm(h, p, t, GX, s->ws, sy, st, (int)off))) return rc;
   int published = 0;
   auto publish = [&](int64_t rows_ready) -> int {  // ready[c] for every chunk whose steps are all available
-    while (published < t.nch && t.seq_end[published] <= rows_ready)
-      HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published++), sy.epoch, 0));
+    for (; published < t.nch && t.seq_end[published] <= rows_ready; ++published)
+      if (published != h->test_drop_ready) HIPCHK(hipStreamWriteValue32(st, (void*)(sy.ready + published), sy.epoch, 0));
     return VAP_OK;
   };
   if (s->pushes > 0 && s->keep1 > s->keep0) {
@@ -1954,12 +1967,8 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);
-  for (auto& kv : h->params) {
-    if (hipMalloc(&kv.second.dev, kv.second.numel * sizeof(float)) != hipSuccess) {
-      delete h;
-      return fail(VAP_ERR_HIP, "hipMalloc params");
-    }
-  }
+  // host-only: the schema (vap_num_params / vap_param_info) needs no device; each parameter's device
+  // copy is allocated by its first vap_set_param
   *out = h;
   return VAP_OK;
 }
@@ -1986,6 +1995,7 @@ int vap_set_param(vap_handle* h, const char* key, const float* src, int64_t nume
   if (it->second.numel != numel)
     return fail(VAP_ERR_WEIGHTS, std::string("size mismatch for ") + key + ": expected " +
                                      std::to_string(it->second.numel) + " got " + std::to_string(numel));
+  if (!it->second.dev) HIPCHK(hipMalloc(&it->second.dev, numel * sizeof(float)));
   HIPCHK(hipMemcpyAsync(it->second.dev, src, numel * sizeof(float), hipMemcpyDefault, (hipStream_t)stream));
   it->second.set = true;
   h->finalized = false;
@@ -2283,6 +2293,16 @@ int vap_test_plan(const vap_handle* h, int batch, int64_t n_samples, int64_t* ou
   const int64_t st[] = {p.s1, p.s2, p.s3, p.s4, p.sh};
   for (int i = 0; i < 8; ++i) out[i] = (int64_t)v[i];
   for (int i = 0; i < 5; ++i) out[8 + i] = st[i];
+  return VAP_OK;
+}
+
+int vap_test_xtag(vap_handle* h, int64_t set, int64_t* get) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  if (get) *get = (int64_t)h->xtag;
+  if (set >= 0) {
+    if (set > 0xFFFFFFFFll) return fail(VAP_ERR_INVALID, "tag out of range");
+    h->xtag = (unsigned)set;
+  }
   return VAP_OK;
 }
 

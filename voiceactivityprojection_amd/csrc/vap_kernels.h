@@ -110,7 +110,8 @@ struct LstmSync {
                      // done[c] after it)
   int time_mode;
   int gx_off = 0;    // gate rows form a ring: step t reads gx row (t + gx_off) mod Tn (streaming)
-  unsigned xepoch = 0;  // lstm_pair: launch epoch in the exchange tags (set by launch_lstm_pair)
+  unsigned xtag = 0;  // lstm_pair: exchange tags of this launch are xtag (XCC handshake) .. xtag + Tn (steps);
+                      // strictly above every earlier launch's on the same exchange slots (set by launch_lstm_pair)
   int xplain = 0;       // lstm_pair: exchange stores with the default policy even across XCDs (experiment; the
                         // XCC-id handshake picks that policy by itself when both halves share an XCD)
   int stamp_t0 = 100;   // lstm_pair<ST>: first of the 4 stamped steps (VAP_LSTM_STAMP_T0)
@@ -132,7 +133,7 @@ hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t 
 // exchange buffer it needs for S sequences (zeroed once; tags carry the launch epoch, which must
 // differ between launches that share the buffer), and the workgroups one launch runs
 hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
-                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xepoch);
+                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
 int lstm_pair_workgroups(int S);
@@ -289,6 +290,8 @@ struct HeadsArgs {
   float* vad;
   int out_T = 0;   // frames per clip of logits / vad (0: T); a frame range's rows go to clip * out_T + out_f0 + t
   int out_f0 = 0;
+  const float* xf = nullptr;  // fp32 rows of the same x (layout of x): the VAD head reads them (the reference's
+                              // va_classifier takes fp32 x, model.py:257-259); null: the bf16 panels
 };
 hipError_t launch_heads(const HeadsArgs& g, hipStream_t st);
 hipError_t read_block_stamps(unsigned long long* out);

@@ -315,33 +315,44 @@ class VapGPT(nn.Module):
 
     @torch.no_grad()
     def probs(self, waveform: Tensor, vad: Optional[Tensor] = None, now_lims: List[int] = [0, 1],
-              future_lims: List[int] = [2, 3]) -> Dict[str, Tensor]:
+              future_lims: List[int] = [2, 3], *, out: Optional[Dict[str, Tensor]] = None) -> Dict[str, Tensor]:
         """vap/model.py:180-225, including quirk Q1: labels always come from the model's own sigmoid
-        VAD (the ``vad`` argument is shadowed), so ``loss`` is always returned."""
-        out = self(waveform)
-        logits, vad_logits = out["logits"], out["vad"]
+        VAD (the ``vad`` argument is shadowed), so ``loss`` is always returned.
+
+        ``out`` (engine extension, keyword only): preallocated contiguous fp32 device tensors for any of
+        the six outputs (e.g. views into one packed buffer that a single collective then ships,
+        ``distributed.PackedOutputs``); the missing ones are allocated.  The results are returned in
+        the same tensors."""
+        fw = self(waveform)
+        logits, vad_logits = fw["logits"], fw["vad"]
         B, T, C = logits.shape
         dev = logits.device
-        probs = torch.empty_like(logits)
-        vad = torch.empty(B, T, 2, device=dev)
-        p_now = torch.empty(B, T, 2, device=dev)
-        p_future = torch.empty(B, T, 2, device=dev)
-        H = torch.empty(B, T, device=dev)
-        st = N.stream_ptr(dev)
         obj = self.objective
         if T - 1 < obj.horizon:  # quirk Q2: the reference fails in unfold
             raise RuntimeError(f"maximum size for tensor at dimension 1 is {T - 1} but size is {obj.horizon}")
         n = T - obj.horizon
+        shapes = {"probs": (B, T, C), "vad": (B, T, 2), "p_now": (B, T, 2), "p_future": (B, T, 2), "H": (B, T),
+                  "loss": (B, n)}
+        res = {}
+        for k, shape in shapes.items():
+            t = out.get(k) if out is not None else None
+            if t is None:
+                t = torch.empty(shape, device=dev, dtype=torch.float32)
+            elif tuple(t.shape) != shape or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():
+                raise ValueError(f"out[{k!r}] must be a contiguous float32 {shape} tensor on {dev}, "
+                                 f"got {tuple(t.shape)} {t.dtype} on {t.device}")
+            res[k] = t
         labels = torch.empty(B, n, dtype=torch.int64, device=dev)
-        loss = torch.empty(B, n, dtype=torch.float32, device=dev)
+        st = N.stream_ptr(dev)
         bf = (ctypes.c_int * obj.n_bins)(*obj.bin_frames)
         # softmax / sigmoid / H / p_now / p_future, then labels from the model's own sigmoid VAD (quirk Q1)
         # and loss_vap (objective.py:209-243) in one call
         N.check(N.lib().vap_probs_loss(logits.data_ptr(), vad_logits.data_ptr(), B, T, obj.n_bins, now_lims[0],
                                        now_lims[-1], future_lims[0], future_lims[1], bf, obj.threshold_ratio,
-                                       probs.data_ptr(), vad.data_ptr(), p_now.data_ptr(), p_future.data_ptr(),
-                                       H.data_ptr(), labels.data_ptr(), loss.data_ptr(), st), "vap_probs_loss")
-        return {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H, "loss": loss}
+                                       res["probs"].data_ptr(), res["vad"].data_ptr(), res["p_now"].data_ptr(),
+                                       res["p_future"].data_ptr(), res["H"].data_ptr(), labels.data_ptr(),
+                                       res["loss"].data_ptr(), st), "vap_probs_loss")
+        return res
 
     @torch.no_grad()
     def vad(self, waveform: Tensor, max_fill_silence_time: float = 0.02, max_omit_spike_time: float = 0.02,

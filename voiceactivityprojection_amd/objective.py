@@ -31,7 +31,10 @@ def _require_device(t: Tensor, what: str) -> None:
 
 
 class ProjectionWindow:
-    """objective.py:14-76 -- kept for API parity (tensor helper)."""
+    """The projection window of objective.py:14-76 as a tensor helper (API parity; the labels of the
+    hot path come from the native ``vap_labels_loss``).  For frame t the window is va[t+1 : t+1+horizon]
+    split into the bins of ``bin_frames``; a bin is active when its mean activity reaches
+    ``threshold_ratio``.  Output (..., n_frames - horizon, 2, n_bins) as float 0/1."""
 
     def __init__(self, bin_times: List = [0.2, 0.4, 0.6, 0.8], frame_hz: int = 50, threshold_ratio: float = 0.5):
         self.bin_times = bin_times
@@ -39,20 +42,18 @@ class ProjectionWindow:
         self.threshold_ratio = threshold_ratio
         self.bin_frames = bin_times_to_frames(bin_times, frame_hz)
         self.n_bins = len(self.bin_frames)
-        self.total_bins = self.n_bins * 2
+        self.total_bins = 2 * self.n_bins
         self.horizon = sum(self.bin_frames)
 
     def projection(self, va: Tensor) -> Tensor:
-        return va[..., 1:, :].unfold(dimension=-2, size=sum(self.bin_frames), step=1)
+        """(..., T, 2) -> (..., T - horizon, 2, horizon): the future frames seen from every frame."""
+        future = va[..., 1:, :]
+        return future.unfold(-2, self.horizon, 1)
 
     def projection_bins(self, projection_window: Tensor) -> Tensor:
-        start, v_bins = 0, []
-        for b in self.bin_frames:
-            end = start + b
-            m = projection_window[..., start:end].sum(dim=-1) / b
-            v_bins.append((m >= self.threshold_ratio).float())
-            start = end
-        return torch.stack(v_bins, dim=-1)
+        sums = torch.stack([part.sum(dim=-1) for part in projection_window.split(self.bin_frames, dim=-1)], dim=-1)
+        lengths = torch.tensor(self.bin_frames, dtype=sums.dtype, device=sums.device)
+        return (sums / lengths >= self.threshold_ratio).to(torch.float32)
 
     def __call__(self, va: Tensor) -> Tensor:
         return self.projection_bins(self.projection(va))

@@ -83,10 +83,14 @@ class VapStream:
                                "create a new stream")
 
     @torch.no_grad()
-    def push(self, audio: Tensor, full: bool = False) -> Dict[str, Tensor]:
+    def push(self, audio: Tensor, full: bool = False, check: bool = True) -> Dict[str, Tensor]:
         """Roll ``audio`` ([B, 2, hop] float32; channels as in ``VapGPT.forward``) into the window and
         return the last ``hop_frames`` frames of probs (B, F, 256), vad, p_now, p_future (B, F, 2) and
-        H (B, F).  ``full=True`` returns every frame of the window plus its ``logits`` / ``vad_logits``."""
+        H (B, F).  ``full=True`` returns every frame of the window plus its ``logits`` / ``vad_logits``.
+
+        ``check=True`` (default) waits for the push and raises if one of its recurrence hand-offs
+        timed out, so no invalid hop is ever returned; ``check=False`` returns without waiting (the
+        failure then surfaces from the next push or :meth:`synchronize`), for pipelined callers."""
         self._check_handle()
         if audio.dim() != 3 or audio.shape[0] != self.batch or audio.shape[1] != 2 or \
                 audio.shape[2] != self.hop_samples:
@@ -109,6 +113,8 @@ class VapStream:
                                   probs.data_ptr(), vad.data_ptr(), p_now.data_ptr(), p_future.data_ptr(),
                                   H.data_ptr(), st), "vap_probs")
         out = {"probs": probs, "vad": vad, "p_now": p_now, "p_future": p_future, "H": H}
+        if check:
+            N.check(N.lib().vap_synchronize(self._h, st), "vap_synchronize")
         if full:
             out["logits"], out["vad_logits"] = logits.clone(), vad_logits.clone()
             return out

@@ -41,23 +41,21 @@ def add_zero_channel(w: Tensor) -> Tensor:
 
 
 def find_island_idx_len(x: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
-    """utils.py:21-49: run-length islands (start index, duration, value)."""
+    """Run-length encoding of a 1-D tensor, as the reference's helper returns it (vap/utils.py:21-49):
+    (start index of every run, its length, its value)."""
     assert x.ndim == 1
-    n = len(x)
-    y = x[1:] != x[:-1]
-    i = torch.cat((torch.where(y)[0], torch.tensor(n - 1, device=x.device).unsqueeze(0))).long()
-    it = torch.cat((torch.tensor(-1, device=x.device).unsqueeze(0), i))
-    dur = it[1:] - it[:-1]
-    idx = torch.cumsum(torch.cat((torch.tensor([0], device=x.device, dtype=torch.long), dur)), dim=0)[:-1]
-    return idx, dur, x[i]
+    values, lengths = torch.unique_consecutive(x, return_counts=True)
+    starts = torch.cumsum(lengths, 0) - lengths
+    return starts, lengths, values
 
 
 def everything_deterministic():
-    """utils.py:52-103. The HIP kernels are deterministic by construction (no float atomics, fixed
-    reduction order); this keeps the reference's global switch for torch code around them."""
-    from os import environ
+    """The reference switches torch to deterministic algorithms at import (vap/utils.py:52-103).  The
+    engine's kernels are deterministic by construction (fixed reduction order, no float atomics);
+    this applies the same switch to any torch code around them."""
+    import os
 
-    environ["CUBLAS_WORKSPACE_CONFIG"] = ":4096:8"
+    os.environ["CUBLAS_WORKSPACE_CONFIG"] = ":4096:8"
     torch.backends.cudnn.deterministic = True
     torch.use_deterministic_algorithms(mode=True)
 
@@ -66,86 +64,82 @@ def batch_to_device(batch, device="cuda"):
     return {k: (v.to(device) if isinstance(v, Tensor) else v) for k, v in batch.items()}
 
 
+def _jsonable(v):
+    if isinstance(v, Tensor):
+        return v.tolist()
+    if isinstance(v, dict):
+        return {k: _jsonable(x) for k, x in v.items()}
+    return v
+
+
 def tensor_dict_to_json(d):
-    new_d = {}
-    for k, v in d.items():
-        if isinstance(v, Tensor):
-            v = v.tolist()
-        elif isinstance(v, dict):
-            v = tensor_dict_to_json(v)
-        new_d[k] = v
-    return new_d
+    """Tensors (also inside nested dicts) -> nested lists, for run.py's JSON (vap/utils.py:116-124)."""
+    return _jsonable(d)
 
 
 def vad_list_to_onehot(vad_list: VAD_LIST, duration: float, hop_time: float = 0, frame_hz: float = 0,
                        channel_first: bool = False) -> Tensor:
-    """utils.py:170-195."""
+    """VAD segment list [[(start, end), ...] per speaker] -> (n_frames, 2) 0/1 frames, a frame being
+    active when it lies in [frame(start), frame(end)) with frame(t) = int(t / hop) (vap/utils.py:170-195)."""
     assert hop_time > 0 or frame_hz > 0, "vad_list_to_onehot requires `frame_hz` or `hop_time`"
-    if frame_hz > 0:
-        hop_time = 1 / frame_hz
-    n_frames = time_to_frames(duration, hop_time)
-    vad_tensor = torch.zeros((n_frames, 2))
-    for ch, ch_vad in enumerate(vad_list):
-        for v in ch_vad:
-            s = time_to_frames(v[0], hop_time)
-            e = time_to_frames(v[1], hop_time)
-            vad_tensor[s:e, ch] = 1.0
-    if channel_first:
-        vad_tensor = vad_tensor.permute(1, 0)
-    return vad_tensor
+    hop = 1 / frame_hz if frame_hz > 0 else hop_time
+    frames = torch.arange(time_to_frames(duration, hop))
+    cols = []
+    for ch in range(2):
+        on = torch.zeros(frames.shape[0], dtype=torch.bool)
+        for seg in (vad_list[ch] if ch < len(vad_list) else []):
+            on |= (frames >= time_to_frames(seg[0], hop)) & (frames < time_to_frames(seg[1], hop))
+        cols.append(on)
+    out = torch.stack(cols, dim=-1).to(torch.float32)
+    return out.t() if channel_first else out
 
 
 def vad_onehot_to_vad_list(vad: Tensor, frame_hz: int = 50, ipu_thresh_time: float = 0.1) -> List[VAD_LIST]:
-    """utils.py:198-236."""
+    """(B, n_frames, 2) 0/1 frames -> per clip and speaker a list of [start, end] seconds (2 decimals);
+    a segment starting less than ``ipu_thresh_time`` after the previous segment's end is merged into
+    it (vap/utils.py:198-236)."""
     assert vad.ndim == 3, f"Expects vad with batch-dim of shape (B, n_frames, 2) but got {vad.shape}"
-    batch_vad_list = []
-    for b in range(vad.shape[0]):
-        vad_list = []
+    result = []
+    for clip in vad:
+        speakers = []
         for ch in range(2):
-            idx, dur, val = find_island_idx_len(vad[b, :, ch])
-            active = idx[val == 1]
-            start_times = active / frame_hz
-            ch_vad_list = []
-            if len(start_times) == 0:
-                vad_list.append(ch_vad_list)
-                continue
-            end_times = start_times + dur[val == 1] / frame_hz
-            start_times, end_times = start_times.tolist(), end_times.tolist()
-            s, last_end = round(start_times[0], 2), round(end_times[0], 2)
-            ch_vad_list.append([s, last_end])
-            for s, e in zip(start_times[1:], end_times[1:]):
-                s, e = round(s, 2), round(e, 2)
-                if s - last_end < ipu_thresh_time:
-                    ch_vad_list[-1][-1] = e
+            starts, lengths, values = find_island_idx_len(clip[:, ch])
+            on = values == 1
+            t0 = (starts[on] / frame_hz).tolist()
+            t1 = (starts[on] / frame_hz + lengths[on] / frame_hz).tolist()
+            segs, prev_end = [], None
+            for a, b in zip(t0, t1):
+                a, b = round(a, 2), round(b, 2)
+                if prev_end is not None and a - prev_end < ipu_thresh_time:
+                    segs[-1][1] = b
                 else:
-                    ch_vad_list.append([s, e])
-                last_end = e
-            vad_list.append(ch_vad_list)
-        batch_vad_list.append(vad_list)
-    return batch_vad_list
+                    segs.append([a, b])
+                prev_end = b
+            speakers.append(segs)
+        result.append(speakers)
+    return result
 
 
-def _fill(vad: Tensor, max_frames: int, value: float) -> Tensor:
-    for ch in range(2):
-        starts, dur, on_off = find_island_idx_len(vad[:, ch])
-        s_ = starts[on_off == (1.0 - value)]
-        d_ = dur[on_off == (1.0 - value)]
-        w = torch.where(d_ <= max_frames)[0]
-        for s, d in zip(s_[w], d_[w]):
-            vad[s: s + d, ch] = value
+def _replace_short_runs(vad: Tensor, max_frames: int, run_value: float, new_value: float) -> Tensor:
+    """In place, per speaker column: every run of ``run_value`` at most ``max_frames`` long becomes
+    ``new_value``."""
+    for ch in range(vad.shape[-1]):
+        _, lengths, values = find_island_idx_len(vad[:, ch])
+        short = (values == run_value) & (lengths <= max_frames)
+        vad[torch.repeat_interleave(short, lengths), ch] = new_value
     return vad
 
 
 def vad_fill_silences(vad: Tensor, max_fill_time: float = 0.02, frame_hz: float = 50) -> Tensor:
-    """utils.py:239-255."""
+    """Silences of at most ``max_fill_time`` become speech (vap/utils.py:239-255)."""
     assert vad.ndim == 2 and vad.shape[-1] == 2, f"Expects (N_FRAMES, 2) got {vad.shape}"
-    return _fill(vad, round(max_fill_time * frame_hz), 1.0)
+    return _replace_short_runs(vad, round(max_fill_time * frame_hz), 0.0, 1.0)
 
 
 def vad_omit_spikes(vad: Tensor, max_omit_time: float = 0.02, frame_hz: float = 50) -> Tensor:
-    """utils.py:258-272."""
+    """Speech spikes of at most ``max_omit_time`` become silence (vap/utils.py:258-272)."""
     assert vad.ndim == 2 and vad.shape[-1] == 2, f"Expects (N_FRAMES, 2) got {vad.shape}"
-    return _fill(vad, round(max_omit_time * frame_hz), 0.0)
+    return _replace_short_runs(vad, round(max_omit_time * frame_hz), 1.0, 0.0)
 
 
 def write_json(data, filename):
