@@ -63,9 +63,13 @@ def test_mono_bf16_batch_vs_oracle():
     hist = torch.rand(B, T, 5, generator=g)
     got = m.probs(wav.cuda(), va.cuda())
     ref = O.probs_mono(wav, va, sd)
-    for k, tol in (("probs", 2e-2), ("p_now", 5e-2), ("p_future", 5e-2), ("H", 1.5e-1)):
-        e = float((got[k].cpu() - ref[k]).abs().max())
-        assert e < tol, f"{k}: {e}"
+    # <= 3x the measured bf16 error of this model (probs 6.8e-3, p_now 2.8e-3, p_future 3.3e-3, H 2.4e-2:
+    # the mono stack runs four plain layers on one speaker, with larger synthetic activations)
+    BF16_TOL = {"probs": 2e-2, "p_now": 8e-3, "p_future": 1e-2, "H": 7e-2}
+    errs = {k: float((got[k].cpu() - ref[k]).abs().max()) for k in ("probs", "p_now", "p_future", "H")}
+    print("mono bf16 max abs err:", errs)
+    bad = {k: e for k, e in errs.items() if not e <= BF16_TOL[k]}
+    assert not bad, bad
     lg = m(wav.cuda(), va.cuda(), hist.cuda())["logits"]
     # batch invariance: each clip alone gives the same logits
     one = m(wav[1:2].cuda(), va[1:2].cuda(), hist[1:2].cuda())["logits"]

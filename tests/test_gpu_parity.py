@@ -17,7 +17,10 @@ from voiceactivityprojection_amd.weights import synthetic_state_dict, synthetic_
 pytestmark = pytest.mark.gpu
 
 FP32_TOL = {"probs": 1e-4, "vad": 1e-4, "p_now": 1e-4, "p_future": 1e-4, "H": 1e-3, "loss": 1e-3}
-BF16_TOL = {"probs": 2e-2, "vad": 3e-2, "p_now": 5e-2, "p_future": 5e-2, "H": 1.5e-1, "loss": 1.5e-1}
+# bf16 perf mode: <= 3x the largest error measured against the reference fixtures (tools/bf16_errors.py,
+# profiles/r3_bf16_errors.json: probs 1.42e-3, vad 1.34e-2, p_now 5.5e-4, p_future 4.8e-4, H 8.9e-3,
+# loss 1.61e-2 over short_clip, example_wav, len_*, batch_20s, bench4_20s, long_60s)
+BF16_TOL = {"probs": 4e-3, "vad": 3e-2, "p_now": 1.5e-3, "p_future": 1.4e-3, "H": 2.5e-2, "loss": 4.5e-2}
 
 
 def _model(precision="fp32", lstm_layers=1):
@@ -220,6 +223,7 @@ def test_encoder_bf16_vs_reference(m16, golden):
     x1, x2 = m16.encode_audio(torch.from_numpy(g["waveform"]).cuda())
     for got, exp in ((x1, g["enc1"]), (x2, g["enc2"])):
         err = (got.cpu().numpy() - exp).__abs__().max()
+        print("bf16 encoder max abs err:", err)
         assert err < 0.08, f"bf16 encoder max abs err {err}"
 
 
@@ -337,6 +341,7 @@ def test_attention_maps_bf16_vs_oracle(m16):
         exp = ref[k].numpy()
         assert got.shape == exp.shape, (k, got.shape, exp.shape)
         err = float(np.abs(got - exp).max())
+        print(f"bf16 attention map {k} max abs err:", err)
         assert err < 3e-2, f"{k}: {err}"
 
 
