@@ -46,12 +46,18 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int M = g.M_per_seq * g.n_seq;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware tile order (1-D grid): blocks b, b + 8, .. share an XCD's L2 (round-robin dealing), so
+  // the N / BN column tiles of one row tile go to consecutive slots of ONE XCD and its A rows are
+  // fetched from HBM once instead of once per column tile
+  const int ntn = g.N / BN;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int mt = (slot / ntn) * 8 + xcd;
+  if (mt * BM >= M) return;  // padding block (whole workgroup, before any barrier)
+  const int m0 = mt * BM, n0 = (slot % ntn) * BN;
   const bf16* __restrict__ A = (const bf16*)g.A;
   const bf16* __restrict__ W = (const bf16*)g.W;
-  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && blockIdx.y == 0 && (lane == 0) &&
-                    (wave == 0 || wave == 4))
-                       ? (int)(blockIdx.x >> 6)
+  const int samp = (ST && (mt & 63) == 0 && mt < 512 && n0 == 0 && (lane == 0) && (wave == 0 || wave == 4))
+                       ? (int)(mt >> 6)
                        : -1;
   auto stamp = [&](int kt, int k) {
     if constexpr (ST) {
@@ -291,7 +297,8 @@ hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
   // 16-byte alignment of every DMA source / epilogue vector access
   if (g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 || (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)))
     return hipErrorInvalidValue;
-  dim3 grid((M + BM - 1) / BM, g.N / BN);
+  const int mtiles = (M + BM - 1) / BM;
+  const dim3 grid((unsigned)((mtiles + 7) / 8 * 8 * (g.N / BN)));  // XCD-aware 1-D order (see the kernel)
   static const bool stamps = getenv("VAP_GEMM2_STAMPS") != nullptr;
   if (stamps)
     hipLaunchKernelGGL((gemm2_kernel<TOut, true>), grid, dim3(512), 0, st, g);

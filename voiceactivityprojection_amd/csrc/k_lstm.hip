@@ -498,16 +498,15 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     }
   }
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + u0;
+  // gate rows with permuted columns (gx_col): this lane's 16 gate values (4 gates x units u0 .. u0+3) of a
+  // step are 32 contiguous bytes, the 4 lane groups of a sequence one 128-byte line
+  const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + gx_col(0, u0);
   const int goff = sync.gx_off;
   auto grow = [&](int t) -> int64_t {
     const int r = t + goff;
     return (int64_t)(r >= Tn ? r - Tn : r) * G4;
   };
-  bf16x4 gn[4];
   __syncthreads();  // hb zeroed; ready acquired
-#pragma unroll
-  for (int g = 0; g < 4; ++g) gn[g] = *(const bf16x4*)(gxs + grow(0) + g * HD);
 
   auto hfrag = [&](int kk) -> chunk16 {  // B operand: h[32kk + 8(lane>>4) + e][seq lane&15]
     return *(const chunk16*)(hb + sl * 512 + (((kk * 4 + (lane >> 4)) ^ sl) << 4));
@@ -533,25 +532,22 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   // are counted by hand: vmcnt retires in issue order, and the compiler's own accounting falls back to
   // vmcnt(0) at the loop's merge points, which would make each exchange wait also wait for the gx
   // prefetch just issued.  Per step t (steady state):
-  //   P  exchange poll (partner's h_{t-1}, t > 0) | G  gx rows of step t+2 (4 loads) | R  poll retries
+  //   P  exchange poll (partner's h_{t-1}, t > 0) | G  gx record of step t+2 (2 loads) | R  poll retries
   //   X  exchange publish (h_t)                   | O  h_t row store
-  // -> the poll wait is vmcnt(4) (G may stay in flight); gx of step t (issued in step t-2) is waited
-  // with vmcnt(9) (at least R X O + P G R X O are younger).  Retries only add younger ops, so both
+  // -> the poll wait is vmcnt(2) (G may stay in flight); gx of step t (issued in step t-2) is waited
+  // with vmcnt(7) (at least R X O + P G R X O are younger).  Retries only add younger ops, so both
   // waits stay sufficient.
   const __amdgpu_buffer_rsrc_t orsc =
       make_rsrc(out + (int64_t)grp * NS * out_seq_stride, (uint32_t)((int64_t)min(NS, S - grp * NS) * out_seq_stride * 2));
   const uint32_t o_lane = (uint32_t)(((int64_t)sl * out_seq_stride + u0) * 2);  // lanes of missing sequences: out of range
-  auto gload = [&](u32x2 (&gv)[4], int row) {
+  auto gload = [&](u32x4 (&gv)[2], int row) {  // gates 0/1 and 2/3 of the lane's 4 units
     const bf16* a = gxs + grow(row);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(gv[g]) : "v"(a + g * HD) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[0]) : "v"(a) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(gv[1]) : "v"(a) : "memory");
   };
-  u32x2 ga[4], gb[4];  // gx ring: ga for even steps, gb for odd
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    ga[g] = __builtin_bit_cast(u32x2, gn[g]);
-    gb[g] = *(const u32x2*)(gxs + grow(Tn > 1 ? 1 : 0) + g * HD);
-  }
+  u32x4 ga[2], gb[2];  // gx ring: ga for even steps, gb for odd
+  gload(ga, 0);
+  gload(gb, Tn > 1 ? 1 : 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // XCD handshake: the exchange stores may stay in the XCD's L2 (default policy instead of
   // write-through: +1.7 % end to end) only when both halves of the pair run on the same XCD, which
@@ -587,15 +583,16 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   }
   auto run = [&](auto half) {
   constexpr int kown = 4 * decltype(half)::value, krem = 4 - kown;
-  auto step = [&](const int t, u32x2 (&gc)[4], u32x2 (&go)[4]) {
+  auto step = [&](const int t, u32x4 (&gc)[2], u32x4 (&go)[2]) {
     stamp(t, 0);
     __builtin_amdgcn_sched_barrier(0);
-    if (t >= 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // gc (gx of step t) landed
+    if (t >= 2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // gc (gx of step t) landed
     stamp(t, 1);
     f32x4 acc[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const bf16x4 v = __builtin_bit_cast(bf16x4, gc[g]);
+      const u32x4 q = gc[g >> 1];
+      const bf16x4 v = __builtin_bit_cast(bf16x4, (g & 1) ? u32x2{q[2], q[3]} : u32x2{q[0], q[1]});
       acc[g] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
     }
     // the partner's h_{t-1}: issue the poll now, consume it after the own-unit k-steps
@@ -613,7 +610,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     stamp(t, 2);
     if (t > 0) {
       __builtin_amdgcn_sched_barrier(0);  // the own-unit MFMAs stay ahead of the wait
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // P landed (G may still be in flight)
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // P landed (G may still be in flight)
       const uint32_t want = tag_base + (uint32_t)(t - 1);
       uint64_t t0 = 0;
       while (!dead && !sync.xnowait && !__all(xv[1] == want && xv[3] == want)) {
@@ -750,15 +747,27 @@ __global__ void pack_whh_pair_kernel(const float* __restrict__ whh, bf16* __rest
   }
 }
 
-// W_ih [1024][256] fp32 -> bf16 with the gate-row scales; b = (b_ih + b_hh) * scale
+// W_ih [1024][256] fp32 -> bf16 with the gate-row scales and the rows in the permuted gate-column order
+// of the pair recurrence (gx_col): the projection GEMM then writes gate rows the recurrence reads as one
+// 32-byte record per lane; b = (b_ih + b_hh) * scale, permuted alike
 __global__ void pack_wih_prescaled_kernel(const float* __restrict__ wih, bf16* __restrict__ out,
                                           const float* __restrict__ bih, const float* __restrict__ bhh,
                                           float* __restrict__ b) {
   const int64_t n = (int64_t)G4 * HD;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int row = (int)(i / HD);
-    out[i] = (bf16)(wih[i] * gate_scale(row));
-    if (i < G4) b[i] = (bih[i] + bhh[i]) * gate_scale((int)i);
+    const int row = (int)(i / HD), k = (int)(i % HD);
+    const int col = gx_col(row >> 8, row & 255);
+    out[(int64_t)col * HD + k] = (bf16)(wih[i] * gate_scale(row));
+    if (i < G4) b[gx_col((int)i >> 8, (int)i & 255)] = (bih[i] + bhh[i]) * gate_scale((int)i);
+  }
+}
+
+// [S][Tn][1024] gate rows in the natural order -> the permuted column order (kernel tests)
+__global__ void permute_gx_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int64_t rows) {
+  const int64_t n = rows * G4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int col = (int)(i & (G4 - 1));
+    out[(i - col) + gx_col(col >> 8, col & 255)] = in[i];
   }
 }
 
@@ -768,6 +777,11 @@ __global__ void scale_gates_kernel(const bf16* __restrict__ in, bf16* __restrict
 }
 
 }  // namespace
+
+hipError_t launch_permute_gx(const bf16* in, bf16* out, int64_t rows, hipStream_t st) {
+  hipLaunchKernelGGL(permute_gx_kernel, dim3(1024), dim3(256), 0, st, in, out, rows);
+  return hipGetLastError();
+}
 
 // gx rows [.][1024] -> the pre-scaled gate units of lstm_cell<true> (kernel tests)
 hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st) {

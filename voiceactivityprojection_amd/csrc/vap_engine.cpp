@@ -96,9 +96,7 @@ struct vap_handle {
   // next call on the handle, vap_synchronize right away)
   unsigned* err_host = nullptr;
   unsigned* err_dev = nullptr;
-  // recurrence split over workgroup pairs (k_lstm.hip lstm_pair_kernel; VAP_LSTM_PAIR=0: one CU per
-  // 16 sequences, lstm_resident_kernel): its exchange buffer and launch epoch (exchange tags)
-  bool lstm_pair = true;
+  // bf16 recurrence: split over workgroup pairs (k_lstm.hip lstm_pair_kernel, two CUs per 16 sequences)
   // conv2..4 on the slab-staged k4 s2 kernel (k_conv234.hip); VAP_CONVK4=0: implicit GEMMs on gemm2
   bool convk4 = true;
   void* xbuf = nullptr;
@@ -497,18 +495,18 @@ int pack_all(vap_handle* h, hipStream_t st) {
   for (int l = 0; l < h->dims.lstm_layers; ++l) {
     const std::string p = "encoder.encoder.gAR.baseNet.", s = "_l" + std::to_string(l);
     T* wih = alloc("wih" + s, 4 * D * D);
-    T* whh = alloc("whh" + s, 4 * D * D);
     float* b = nullptr;
-    if (!wih || !whh || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
+    if (!wih || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
     h->fpacked["bias" + s] = b;
-    if constexpr (sizeof(T) == 2) {  // resident bf16 recurrence: gate scales folded into the weights
+    if constexpr (sizeof(T) == 2) {  // bf16 pair recurrence: gate scales folded into the weights, gx_col order
       HIPCHK(launch_pack_wih_prescaled(h->P(p + "weight_ih" + s), (bf16*)wih, h->P(p + "bias_ih" + s),
                                        h->P(p + "bias_hh" + s), b, st));
-      HIPCHK(launch_pack_whh_resident(h->P(p + "weight_hh" + s), (bf16*)whh, st, true));
       T* whp = alloc("whh_pair" + s, 4 * D * D);  // the pair split's layout (lstm_pair_kernel)
       if (!whp) return fail(VAP_ERR_HIP, "hipMalloc lstm");
       HIPCHK(launch_pack_whh_pair(h->P(p + "weight_hh" + s), (bf16*)whp, st));
     } else {
+      T* whh = alloc("whh" + s, 4 * D * D);
+      if (!whh) return fail(VAP_ERR_HIP, "hipMalloc lstm");
       HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
       HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
       HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
@@ -1088,25 +1086,21 @@ static int lstm_wg_cap(const vap_handle* h) {
   return h->lstm_max_wg > 0 ? h->lstm_max_wg : std::max(1, device_cus() / 2);
 }
 // workgroups of one bf16 recurrence launch over S sequences (each publishes done counters)
-static int rec_workgroups(const vap_handle* h, int S) { return h->lstm_pair ? lstm_pair_workgroups(S) : (S + 15) / 16; }
+static int rec_workgroups(const vap_handle*, int S) { return lstm_pair_workgroups(S); }
 // groups of 16 sequences one persistent launch may take (at least one, whatever the cap)
-static int rec_group_cap(const vap_handle* h) { return std::max(1, lstm_wg_cap(h) / (h->lstm_pair ? 2 : 1)); }
+static int rec_group_cap(const vap_handle* h) { return std::max(1, lstm_wg_cap(h) / 2); }
 static bool persistent_fits(const vap_handle* h, int S) { return (S + 15) / 16 <= rec_group_cap(h); }
 // workgroups of a persistent conv launch: the CUs the recurrence running beside it leaves free
 static int conv_grid_cap(const vap_handle* h, int S) {
   return device_cus() - std::min(rec_workgroups(h, S), lstm_wg_cap(h));
 }
 
-// The bf16 recurrence of S sequences (gate rows GX [S][L4][1024], h rows to out): the pair split
-// (default) or the single-CU resident kernel.  xg0 offsets the launch's slots in the exchange buffer
-// (launches that may run concurrently use disjoint slots).
+// The bf16 recurrence of S sequences (gate rows GX [S][L4][1024] in the gx_col column order, h rows to
+// out) on the pair-split kernel.  xg0 offsets the launch's slots in the exchange buffer (launches that
+// may run concurrently use disjoint slots).
 int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* out, int64_t out_stride, hipStream_t st,
                const LstmSync* sy, int xg0) {
   const std::string s = "_l" + std::to_string(layer);
-  if (!h->lstm_pair) {
-    HIPCHK(launch_lstm_resident(GX, S, L4, h->W<bf16>("whh" + s), out, out_stride, st, sy, true));
-    return VAP_OK;
-  }
   const size_t slot = lstm_pair_xbuf_bytes(16);
   const size_t need = (size_t)xg0 * slot + lstm_pair_xbuf_bytes(S);
   if (need > h->xbuf_bytes) {  // grow (rare): nothing may still use the old buffer
@@ -1598,7 +1592,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       sy.nr = nr;
       for (int i = 0; i < nr; ++i) sy.seq_end[i] = 2 * (rs[i].c0 + rs[i].nc);
       unsigned add[vap_handle::MAXMB] = {};
-      const unsigned per_grp = h->lstm_pair ? 2u : 1u;  // workgroups per 16 sequences
+      const unsigned per_grp = 2u;  // workgroups per 16 sequences (pair split)
       for (int wg = 0; wg * 16 < S; ++wg) {  // done increments per range (16 sequences per group)
         const int s_first = wg * 16, s_last = std::min(S, s_first + 16) - 1;
         int ra = 0;
@@ -1937,7 +1931,6 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
-  if (const char* e = getenv("VAP_LSTM_PAIR")) h->lstm_pair = atoi(e) != 0;
   if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();

@@ -136,6 +136,12 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
                             hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
+// Column of gate row (g, u) (gate g, hidden unit u) in the bf16 gate buffer of the pair recurrence: the
+// 16 values of 4 gates x 4 consecutive units (one recurrence lane's) are 32 contiguous bytes, the 4 lane
+// groups of a wave's sequence one 128-byte line (W_ih / bias rows are packed in this order)
+__host__ __device__ inline int gx_col(int g, int u) { return (u >> 2) * 16 + g * 4 + (u & 3); }
+// [rows][1024] natural gate order -> gx_col order (kernel tests)
+hipError_t launch_permute_gx(const bf16* in, bf16* out, int64_t rows, hipStream_t st);
 int lstm_pair_workgroups(int S);
 hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st);
 hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,
