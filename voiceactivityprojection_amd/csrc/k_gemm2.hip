@@ -52,8 +52,13 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   const int ntn = g.N / BN;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int mt = (slot / ntn) * 8 + xcd;
-  if (mt * BM >= M) return;  // padding block (whole workgroup, before any barrier)
+  // c_pair (LSTM gate projection into the pair-recurrence layout): a tile is 16 steps x 16 sequences,
+  // tile row r = sequence 16 pg + r % 16 at step 16 pt + r / 16
+  const int ntb = g.c_pair ? (g.M_per_seq + 15) / 16 : 1;
+  const int mtiles = g.c_pair ? (g.n_seq + 15) / 16 * ntb : (M + BM - 1) / BM;
+  if (mt >= mtiles) return;  // padding block (whole workgroup, before any barrier)
   const int m0 = mt * BM, n0 = (slot % ntn) * BN;
+  const int pg = mt / ntb, pt = mt - pg * ntb;
   const bf16* __restrict__ A = (const bf16*)g.A;
   const bf16* __restrict__ W = (const bf16*)g.W;
   const int samp = (ST && (mt & 63) == 0 && mt < 512 && n0 == 0 && (lane == 0) && (wave == 0 || wave == 4))
@@ -83,9 +88,17 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 16 + (lane >> 2);
     const int c = swz(row, lane & 3);
-    int m = m0 + row;
-    m = m < M ? m : M - 1;  // tail rows: any valid row (never stored)
-    const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+    int s, t;
+    if (g.c_pair) {
+      s = pg * 16 + (row & 15);
+      t = pt * 16 + (row >> 4);
+      if (s >= g.n_seq || t >= g.M_per_seq) s = t = 0;  // tail rows: any valid row (never stored)
+    } else {
+      int m = m0 + row;
+      m = m < M ? m : M - 1;  // tail rows: any valid row (never stored)
+      s = m / g.M_per_seq;
+      t = m - s * g.M_per_seq;
+    }
     aoff[i] = (uint32_t)(((int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * 8) * 2);
     boff[i] = (uint32_t)(((int64_t)(n0 + row) * g.K + c * 8) * 2);
   }
@@ -264,6 +277,30 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   }
   tstamp(3);
   TOut* __restrict__ C = (TOut*)g.C;
+  if (g.c_pair) {  // gate rows into the pair-recurrence layout: the lane's 4 column blocks are the 4 gates of
+                   // units 16ub + 4fc .. +3 (W rows in gx_wrow order), i.e. one whole record of 2 x 16 bytes
+    const int ub = (n0 + wn * 64) >> 6;
+    const int s = pg * 16 + fr;
+    if (s < g.n_seq) {
+      const int gsq = g.c_s0 + s;
+      const int64_t lo = (int64_t)((fc * 16 + (gsq & 15)) * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = pt * 16 + wm * 8 + i;
+        if (t >= g.M_per_seq) continue;
+        int sl = g.c_t0 + t;
+        sl = sl >= g.c_tn ? sl - g.c_tn : sl;
+        bf16* rec = (bf16*)C + gx_pair_block(gsq >> 4, sl, ub, g.c_tn) + lo;
+        const u32x2 a0 = pack_bf16x4(acc[0][i][0], acc[0][i][1], acc[0][i][2], acc[0][i][3]);
+        const u32x2 a1 = pack_bf16x4(acc[1][i][0], acc[1][i][1], acc[1][i][2], acc[1][i][3]);
+        const u32x2 a2 = pack_bf16x4(acc[2][i][0], acc[2][i][1], acc[2][i][2], acc[2][i][3]);
+        const u32x2 a3 = pack_bf16x4(acc[3][i][0], acc[3][i][1], acc[3][i][2], acc[3][i][3]);
+        *(u32x4*)rec = u32x4{a0[0], a0[1], a1[0], a1[1]};
+        *(u32x4*)(rec + 512) = u32x4{a2[0], a2[1], a3[0], a3[1]};
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + fr;
@@ -297,7 +334,10 @@ hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
   // 16-byte alignment of every DMA source / epilogue vector access
   if (g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 || (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)))
     return hipErrorInvalidValue;
-  const int mtiles = (M + BM - 1) / BM;
+  if (g.c_pair && (sizeof(TOut) != 2 || g.N != 1024 || g.norm || g.act || g.add || g.c_tn <= 0 || g.c_t0 < 0 ||
+                   g.c_t0 >= g.c_tn || g.M_per_seq > g.c_tn || g.c_s0 < 0))
+    return hipErrorInvalidValue;
+  const int mtiles = g.c_pair ? (g.n_seq + 15) / 16 * ((g.M_per_seq + 15) / 16) : (M + BM - 1) / BM;
   const dim3 grid((unsigned)((mtiles + 7) / 8 * 8 * (g.N / BN)));  // XCD-aware 1-D order (see the kernel)
   static const bool stamps = getenv("VAP_GEMM2_STAMPS") != nullptr;
   if (stamps)

@@ -441,7 +441,7 @@ __device__ unsigned long long g_lstm_handoff[1 + 3 * 16];
 __device__ unsigned g_lstm_xcc[64];  // block b < 64 of the last launch: own XCC | partner's << 8 | L2 exchange << 16 | 1 << 24
 
 template <bool PRE, bool ST>
-__global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restrict__ gx, int S, int Tn,
+__global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restrict__ gx, int seq0, int S, int Tn,
                                                           const chunk16* __restrict__ wp, bf16* __restrict__ out,
                                                           int64_t out_seq_stride, LstmSync sync, u32x4* xbuf) {
   __shared__ __attribute__((aligned(16))) unsigned char hb[NS * 512];  // h_{t-1} [seq][256], chunk ^= seq
@@ -498,13 +498,15 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     }
   }
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  // gate rows with permuted columns (gx_col): this lane's 16 gate values (4 gates x units u0 .. u0+3) of a
-  // step are 32 contiguous bytes, the 4 lane groups of a sequence one 128-byte line
-  const bf16* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + gx_col(0, u0);
+  // gate rows in the pair layout (gx_pair_block): this lane's 16 gate values (4 gates x units u0 .. u0+3)
+  // of a step are two 16-byte halves, each wave-load one contiguous KiB (a launch starting mid-group, seq0
+  // % 16 != 0, splits it over two blocks; missing sequences read sequence seq0's records)
+  const int gs = seq0 + (valid ? seq : 0);
+  const bf16* gxs = gx + gx_pair_block(gs >> 4, 0, u0 >> 4, Tn) + (((u0 >> 2) & 3) * 16 + (gs & 15)) * 8;
   const int goff = sync.gx_off;
-  auto grow = [&](int t) -> int64_t {
+  auto grow = [&](int t) -> int64_t {  // slot stride of a group: 16 blocks of 1024 elements
     const int r = t + goff;
-    return (int64_t)(r >= Tn ? r - Tn : r) * G4;
+    return (int64_t)(r >= Tn ? r - Tn : r) * (16 * 1024);
   };
   __syncthreads();  // hb zeroed; ready acquired
 
@@ -543,7 +545,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   auto gload = [&](u32x4 (&gv)[2], int row) {  // gates 0/1 and 2/3 of the lane's 4 units
     const bf16* a = gxs + grow(row);
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[0]) : "v"(a) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(gv[1]) : "v"(a) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(gv[1]) : "v"(a) : "memory");
   };
   u32x4 ga[2], gb[2];  // gx ring: ga for even steps, gb for odd
   gload(ga, 0);
@@ -747,27 +749,28 @@ __global__ void pack_whh_pair_kernel(const float* __restrict__ whh, bf16* __rest
   }
 }
 
-// W_ih [1024][256] fp32 -> bf16 with the gate-row scales and the rows in the permuted gate-column order
-// of the pair recurrence (gx_col): the projection GEMM then writes gate rows the recurrence reads as one
-// 32-byte record per lane; b = (b_ih + b_hh) * scale, permuted alike
+// W_ih [1024][256] fp32 -> bf16 with the gate-row scales and the rows in the gx_wrow order of the c_pair
+// gate projection (its lanes then hold whole records of the pair layout); b = (b_ih + b_hh) * scale,
+// permuted alike
 __global__ void pack_wih_prescaled_kernel(const float* __restrict__ wih, bf16* __restrict__ out,
                                           const float* __restrict__ bih, const float* __restrict__ bhh,
                                           float* __restrict__ b) {
   const int64_t n = (int64_t)G4 * HD;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(i / HD), k = (int)(i % HD);
-    const int col = gx_col(row >> 8, row & 255);
+    const int col = gx_wrow(row >> 8, row & 255);
     out[(int64_t)col * HD + k] = (bf16)(wih[i] * gate_scale(row));
-    if (i < G4) b[gx_col((int)i >> 8, (int)i & 255)] = (bih[i] + bhh[i]) * gate_scale((int)i);
+    if (i < G4) b[gx_wrow((int)i >> 8, (int)i & 255)] = (bih[i] + bhh[i]) * gate_scale((int)i);
   }
 }
 
-// [S][Tn][1024] gate rows in the natural order -> the permuted column order (kernel tests)
-__global__ void permute_gx_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int64_t rows) {
-  const int64_t n = rows * G4;
+// [S][Tn][1024] gate rows in the natural order -> the pair layout (kernel tests)
+__global__ void pack_gx_pair_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int S, int Tn) {
+  const int64_t n = (int64_t)S * Tn * G4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int col = (int)(i & (G4 - 1));
-    out[(i - col) + gx_col(col >> 8, col & 255)] = in[i];
+    const int64_t r = i >> 10;
+    out[gx_pair_off((int)(r / Tn), (int)(r % Tn), col >> 8, col & 255, Tn)] = in[i];
   }
 }
 
@@ -778,8 +781,8 @@ __global__ void scale_gates_kernel(const bf16* __restrict__ in, bf16* __restrict
 
 }  // namespace
 
-hipError_t launch_permute_gx(const bf16* in, bf16* out, int64_t rows, hipStream_t st) {
-  hipLaunchKernelGGL(permute_gx_kernel, dim3(1024), dim3(256), 0, st, in, out, rows);
+hipError_t launch_pack_gx_pair(const bf16* in, bf16* out, int S, int Tn, hipStream_t st) {
+  hipLaunchKernelGGL(pack_gx_pair_kernel, dim3(1024), dim3(256), 0, st, in, out, S, Tn);
   return hipGetLastError();
 }
 
@@ -828,9 +831,9 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
 size_t lstm_pair_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * P_SLOT * 16; }
 int lstm_pair_workgroups(int S) { return 2 * ((S + NS - 1) / NS); }
 
-hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
-                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag) {
-  if (S <= 0 || Tn <= 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn > 0xFFFFFFFFull)
+hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out,
+                            int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag) {
+  if (S <= 0 || Tn <= 0 || seq0 < 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn > 0xFFFFFFFFull)
     return hipErrorInvalidValue;
   LstmSync sy{};
   if (sync) {
@@ -859,10 +862,10 @@ hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair,
   const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
   static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
   if (stamps)
-    hipLaunchKernelGGL((lstm_pair_kernel<true, true>), grid, dim3(512), 0, st, gx, S, Tn, (const chunk16*)whh_pair, out,
+    hipLaunchKernelGGL((lstm_pair_kernel<true, true>), grid, dim3(512), 0, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
                        out_seq_stride, sy, (u32x4*)xbuf);
   else
-    hipLaunchKernelGGL((lstm_pair_kernel<true, false>), grid, dim3(512), 0, st, gx, S, Tn, (const chunk16*)whh_pair, out,
+    hipLaunchKernelGGL((lstm_pair_kernel<true, false>), grid, dim3(512), 0, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
                        out_seq_stride, sy, (u32x4*)xbuf);
   return hipGetLastError();
 }

@@ -314,7 +314,8 @@ Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross
   p.X2 = take(S * p.s2 * es);
   p.X3 = take(S * p.s3 * es);
   p.X4 = take(S * p.s4 * es);
-  p.GX = take(S * p.L[4] * 4 * D * sizeof(float));
+  // gate rows: fp32 [S][L4][1024], or bf16 in the pair-recurrence layout (whole groups of 16 sequences)
+  p.GX = take(std::max<int64_t>(S * 4, (S + 15) / 16 * 16 * 2) * p.L[4] * 4 * D);
   p.H0 = take(S * p.sh * es);
   p.H1 = take(S * p.sh * es);
   p.X = take(S * T * D * sizeof(float));
@@ -498,7 +499,7 @@ int pack_all(vap_handle* h, hipStream_t st) {
     float* b = nullptr;
     if (!wih || hipMalloc(&b, 4 * D * sizeof(float)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
     h->fpacked["bias" + s] = b;
-    if constexpr (sizeof(T) == 2) {  // bf16 pair recurrence: gate scales folded into the weights, gx_col order
+    if constexpr (sizeof(T) == 2) {  // bf16 pair recurrence: gate scales folded in, rows in gx_wrow order
       HIPCHK(launch_pack_wih_prescaled(h->P(p + "weight_ih" + s), (bf16*)wih, h->P(p + "bias_ih" + s),
                                        h->P(p + "bias_hh" + s), b, st));
       T* whp = alloc("whh_pair" + s, 4 * D * D);  // the pair split's layout (lstm_pair_kernel)
@@ -816,8 +817,8 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   return VAP_OK;
 }
 
-int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* out, int64_t out_stride, hipStream_t st,
-               const LstmSync* sy, int xg0);
+int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer, bf16* out, int64_t out_stride,
+               hipStream_t st, const LstmSync* sy, int xg0);
 
 // LSTM layer l of a clip range: input projection GEMM on `st`, recurrence on `rec_st`
 // (bf16 mode: gx bf16, W_hh resident on the CU).
@@ -830,13 +831,20 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
   T* X4 = (T*)(ws + p.X4) + r.s0() * p.s4;
   T* Hb[2] = {(T*)(ws + p.H0) + r.s0() * p.sh, (T*)(ws + p.H1) + r.s0() * p.sh};
   constexpr bool bf = sizeof(T) == 2;
-  void* GX = bf ? (void*)((bf16*)(ws + p.GX) + r.s0() * L4 * 4 * D) : (void*)((float*)(ws + p.GX) + r.s0() * L4 * 4 * D);
+  // bf16: the whole batch's gate buffer in the pair-recurrence layout, this range from sequence r.s0()
+  void* GX = bf ? (void*)(ws + p.GX) : (void*)((float*)(ws + p.GX) + r.s0() * L4 * 4 * D);
   const T* in = l == 0 ? X4 + D : Hb[(l - 1) & 1] + 4 * D;
   const int64_t in_seq = l == 0 ? p.s4 : p.sh;
   {
     Timed tm(h, VAP_K_LSTM_PROJ, st);
-    HIPCHK(gemm<T>(gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L4, S, GX, 4 * D,
-                         L4 * 4 * D), st, !bf));
+    GemmArgs ga = gargs(in, D, in_seq, h->W<T>("wih" + s), D, 4 * D, h->fpacked.at("bias" + s), (int)L4, S, GX, 4 * D,
+                        L4 * 4 * D);
+    if (bf) {
+      ga.c_pair = 1;
+      ga.c_s0 = r.s0();
+      ga.c_tn = (int)L4;
+    }
+    HIPCHK(gemm<T>(ga, st, !bf));
   }
   if (!recurrence) return VAP_OK;
   if (rec_st != st) {  // fork: the recurrence waits for the projection (ONE event from the pool)
@@ -847,7 +855,8 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
   {
     Timed tm(h, VAP_K_LSTM_REC, rec_st);
     if constexpr (bf) {
-      if (int rc = launch_rec(h, (const bf16*)GX, S, (int)L4, l, (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr, xg0))
+      if (int rc = launch_rec(h, (const bf16*)GX, r.s0(), S, (int)L4, l, (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr,
+                              xg0))
         return rc;
     } else
       HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
@@ -1095,11 +1104,11 @@ static int conv_grid_cap(const vap_handle* h, int S) {
   return device_cus() - std::min(rec_workgroups(h, S), lstm_wg_cap(h));
 }
 
-// The bf16 recurrence of S sequences (gate rows GX [S][L4][1024] in the gx_col column order, h rows to
+// The bf16 recurrence of S sequences (gate rows: the pair-layout buffer GX from sequence seq0, h rows to
 // out) on the pair-split kernel.  xg0 offsets the launch's slots in the exchange buffer (launches that
 // may run concurrently use disjoint slots).
-int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* out, int64_t out_stride, hipStream_t st,
-               const LstmSync* sy, int xg0) {
+int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer, bf16* out, int64_t out_stride,
+               hipStream_t st, const LstmSync* sy, int xg0) {
   const std::string s = "_l" + std::to_string(layer);
   const size_t slot = lstm_pair_xbuf_bytes(16);
   const size_t need = (size_t)xg0 * slot + lstm_pair_xbuf_bytes(S);
@@ -1121,7 +1130,7 @@ int launch_rec(vap_handle* h, const bf16* GX, int S, int L4, int layer, bf16* ou
   }
   const unsigned tag0 = h->xtag + 1;  // this launch: tags tag0 .. tag0 + L4
   h->xtag += (unsigned)span;
-  HIPCHK(launch_lstm_pair(GX, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
+  HIPCHK(launch_lstm_pair(GX, seq0, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
                           (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0));
   return VAP_OK;
 }
@@ -1247,7 +1256,7 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
   {
     Timed tm(h, VAP_K_LSTM_REC, side);
-    if (int rc = launch_rec(h, GX, p.S, (int)p.L[4], 0, (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
+    if (int rc = launch_rec(h, GX, 0, p.S, (int)p.L[4], 0, (bf16*)(ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
   }
   // the back ends wait for these counts: raise them only once the launch is in the queue (a failed
   // launch must not leave later forwards waiting for arrivals that never come)
@@ -1453,8 +1462,12 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   for (int64_t r = a4; r < b4;) {
     const int64_t slot = (r + gx_off) % L[4];
     const int64_t n = std::min(b4 - r, L[4] - slot);
-    HIPCHK(gemm<T>(gargs(Xs[3] + D + r * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)n, S,
-                         GX + slot * 4 * D, 4 * D, L[4] * 4 * D), st, false));
+    GemmArgs ga = gargs(Xs[3] + D + r * D, D, p.s4, h->W<T>("wih_l0"), D, 4 * D, h->fpacked.at("bias_l0"), (int)n, S,
+                        GX, 4 * D, L[4] * 4 * D);
+    ga.c_pair = 1;  // the pair-recurrence layout, ring slots slot .. slot + n - 1
+    ga.c_t0 = (int)slot;
+    ga.c_tn = (int)L[4];
+    HIPCHK(gemm<T>(ga, st, false));
     r += n;
   }
   return VAP_OK;
@@ -1607,7 +1620,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
       HIPCHK(hipStreamWaitEvent(side, fork, 0));
       {
         Timed tm(h, VAP_K_LSTM_REC, side);
-        if ((rc = launch_rec(h, (const bf16*)(ws + p.GX), S, (int)L[4], 0, (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh,
+        if ((rc = launch_rec(h, (const bf16*)(ws + p.GX), 0, S, (int)L[4], 0, (bf16*)((T*)(ws + p.H0) + 4 * D), p.sh,
                              side, &sy, 0)))
           return rc;
       }
@@ -1772,7 +1785,7 @@ int stream_push_graph(vap_stream* s, const float* hop_audio, float* logits, floa
   hipEvent_t fork = h->next_fork_event();
   HIPCHK(hipEventRecord(fork, st));
   HIPCHK(hipStreamWaitEvent(side, fork, 0));
-  if (int rc = launch_rec(h, s->gx, S, (int)L4, 0, (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
+  if (int rc = launch_rec(h, s->gx, 0, S, (int)L4, 0, (bf16*)(s->ws + p.H0) + 4 * D, p.sh, side, &sy, 0)) return rc;
   // captured: everything else on the caller's stream
   const vap_stream::GKey key{off, nxt, logits, vadl};
   auto it = s->graphs.find(key);
@@ -2127,7 +2140,7 @@ int vap_stream_create(vap_handle* h, int batch, int64_t window_samples, int64_t 
   s->reuse = bf && h->use_time_chunks() && h->wait_value && hop_samples % 160 == 0 && persistent_fits(h, S);
   if (const char* e = getenv("VAP_STREAM_REUSE")) s->reuse = s->reuse && atoi(e) != 0;  // A/B: 0 = recompute
   if (s->reuse) {
-    if (hipMalloc(&s->gx, (size_t)S * L[4] * 4 * D * sizeof(bf16)) != hipSuccess) return bail("gate buffer");
+    if (hipMalloc(&s->gx, (size_t)gx_pair_elems(S, L[4]) * sizeof(bf16)) != hipSuccess) return bail("gate buffer");
     s->hop_rows = (int)(hop_samples / 160);
     int64_t c0 = 0;
     while (c0 < L[4] && !conv4_row_clean(L, window_samples, c0)) ++c0;

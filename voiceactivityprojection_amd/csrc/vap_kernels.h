@@ -20,6 +20,10 @@ struct GemmArgs {
   float eps;
   int norm;               // 0 none, 1 ChannelNorm (unbiased var), 2 LayerNorm (biased var)
   int act;                // 0 none, 1 relu, 2 gelu(erf)
+  // c_pair = 1 (bf16 LSTM gate projection, N = 1024, W rows in gx_wrow order): C is the gate buffer in the
+  // pair-recurrence layout (gx_pair_block): a tile is 16 time steps x 16 sequences (of sequences
+  // c_s0 + 16k ..), row t of sequence s lands in ring slot (c_t0 + t) mod c_tn; ldc / c_seq_stride unused
+  int c_pair = 0, c_s0 = 0, c_t0 = 0, c_tn = 0;
 };
 
 template <typename T, typename TOut>
@@ -132,16 +136,31 @@ hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t 
 // W_hh split over a pair of workgroups (k_lstm.hip lstm_pair_kernel): pre-scaled packing, the
 // exchange buffer it needs for S sequences (zeroed once; tags carry the launch epoch, which must
 // differ between launches that share the buffer), and the workgroups one launch runs
-hipError_t launch_lstm_pair(const bf16* gx, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
+// gx: the pair-layout gate buffer (gx_pair_block) whose sequence seq0 is this launch's sequence 0
+hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
                             hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
-// Column of gate row (g, u) (gate g, hidden unit u) in the bf16 gate buffer of the pair recurrence: the
-// 16 values of 4 gates x 4 consecutive units (one recurrence lane's) are 32 contiguous bytes, the 4 lane
-// groups of a wave's sequence one 128-byte line (W_ih / bias rows are packed in this order)
-__host__ __device__ inline int gx_col(int g, int u) { return (u >> 2) * 16 + g * 4 + (u & 3); }
-// [rows][1024] natural gate order -> gx_col order (kernel tests)
-hipError_t launch_permute_gx(const bf16* in, bf16* out, int64_t rows, hipStream_t st);
+// The bf16 LSTM gate buffer in the pair-recurrence layout (k_lstm.hip lstm_pair_kernel): for each group of
+// 16 sequences, ring slot and 16-unit block ub = 8p + w (half p of the pair, wave w), one 2 KiB block of
+// 2 halves x 64 lanes x 16 bytes, lane = 16 lg + s % 16 holding units 16ub + 4lg .. +3 of sequence s:
+// half 0 = gates 0, 1 (4 bf16 each), half 1 = gates 2, 3.  A recurrence wave reads its step as two 1 KiB
+// lines-aligned loads, and a gate-projection wave (16 steps x 16 sequences per tile) writes them alike.
+// Element offset of the block:
+__host__ __device__ inline int64_t gx_pair_block(int grp, int slot, int ub, int tn) {
+  return (((int64_t)grp * tn + slot) * 16 + ub) * 1024;
+}
+// element of gate row (g, u) of sequence s, slot `slot`
+__host__ __device__ inline int64_t gx_pair_off(int s, int slot, int g, int u, int tn) {
+  return gx_pair_block(s >> 4, slot, u >> 4, tn) + (g >> 1) * 512 + (((u >> 2) & 3) * 16 + (s & 15)) * 8 + (g & 1) * 4 +
+         (u & 3);
+}
+inline int64_t gx_pair_elems(int S, int64_t Tn) { return (int64_t)((S + 15) / 16) * 16 * Tn * 1024; }
+// W_ih / bias row order of the gate projection in c_pair mode: output column n = 64ub + 16g + (u % 16), so
+// a GEMM lane's 4 column blocks are the 4 gates of its 4 units (one full record)
+__host__ __device__ inline int gx_wrow(int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); }
+// [S][Tn][1024] natural gate order -> the pair layout (kernel tests)
+hipError_t launch_pack_gx_pair(const bf16* in, bf16* out, int S, int Tn, hipStream_t st);
 int lstm_pair_workgroups(int S);
 hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st);
 hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,

@@ -127,10 +127,13 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
     if (e == hipSuccess) e = launch_pack_whh_pair(whh, (bf16*)whh_packed, st);
     if (e == hipSuccess) e = launch_scale_gates((const bf16*)gx, (bf16*)gs, n, st);
     void* gp = nullptr;
-    if (e == hipSuccess && hipMalloc(&gp, n * sizeof(bf16)) != hipSuccess) e = hipErrorOutOfMemory;
-    if (e == hipSuccess) e = launch_permute_gx((const bf16*)gs, (bf16*)gp, (int64_t)S * T, st);  // the engine's order
+    const size_t gpb = gx_pair_elems(S, T) * sizeof(bf16);
+    if (e == hipSuccess && hipMalloc(&gp, gpb) != hipSuccess) e = hipErrorOutOfMemory;
+    if (e == hipSuccess) e = hipMemsetAsync(gp, 0, gpb, st);
+    if (e == hipSuccess) e = launch_pack_gx_pair((const bf16*)gs, (bf16*)gp, S, T, st);  // the engine's layout
     if (e == hipSuccess)
-      e = launch_lstm_pair((const bf16*)gp, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr, xb, 1);
+      e = launch_lstm_pair((const bf16*)gp, 0, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr,
+                           xb, 1);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (gp) (void)hipFree(gp);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
