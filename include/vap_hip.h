@@ -193,19 +193,8 @@ int vap_test_conv0(int precision, const float* wav, int B, int64_t N, int L0, co
 int vap_test_probe_mfma_f32(const float* a, const float* b, float* d, void* stream);
 int vap_test_layernorm(int precision, const float* x, int64_t rows, const float* gamma, const float* beta, void* out,
                        void* raw, void* stream);
-/* row-panel projection GEMM (bf16 perf path, K = 256): amode 0 bf16 A / 1 fp32 A + LayerNorm /
- * 2 fp32 A raw; epi 0 bf16 out / 1 GELU bf16 out / 2 fp32 out + residual `add` (ld = ldc).
- * amode | 16: W is given in the packed row-panel layout [N/256][K/32][16][64][8]. */
-int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
-                      const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream);
-
-/* fused FFN block (bf16 path): x [M][256] fp32 += W2 . GELU(W1 . LayerNorm(x)), W1 [768][256] / W2 [256][768] bf16 */
 /* weight packing into the projection layout [N/256][K/32][16][64][8] (N % 256 == 0, K % 32 == 0) */
 int vap_test_pack_weight(const void* W, void* out, int N, int K, void* stream);
-/* fused FFN block with W1 / W2 already packed (vap_test_pack_weight) */
-int vap_test_ffn_packed(float* x, int M, const void* W1p, const void* W2p, const float* gamma, const float* beta,
-                        void* stream);
-int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream);
 /* fused layer tail (bf16 path): x' = x + o . Wo^T (o [M][256] bf16, skipped when o is NULL), then
  * x = x' + W2 . GELU(W1 . LayerNorm(x')); plain [N][K] bf16 weights; cus picks the rows per workgroup */
 int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W1, const void* W2, const float* gamma,
@@ -215,6 +204,9 @@ int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W
  * cp [M][768] = LN(x) . Wp^T and, nr = 2, cr [M][512] = x . Wr^T from the raw rows */
 int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* Wp, int np, const void* Wr, int nr,
                     void* cp, void* cr, const float* gamma, const float* beta, void* stream);
+/* the same with weights already packed (vap_test_pack_weight): no allocation, no synchronisation */
+int vap_test_lnproj_packed(float* x, const void* o, int M, const void* Wop, const void* Wpp, int np, const void* Wrp,
+                           int nr, void* cp, void* cr, const float* gamma, const float* beta, void* stream);
 /* fused combinator + vap_head (bf16 path, k_block.hip heads_kernel): x bf16 [2B][T][256] (sequences 2b / 2b+1 =
  * the two speakers of clip b), plain [256][256] bf16 Wa / Wb / Wh -> logits [B][T][256] fp32 =
  * (GELU(LN(x1 Wa^T)) + GELU(LN(x2 Wb^T))) Wh^T + hbias, vad [B][T][2] = x1 / x2 . vw + vb */
@@ -236,11 +228,6 @@ int vap_test_read_stamps(unsigned long long* out);
 int vap_test_read_block_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled LN-projection workgroups (VAP_LNPROJ_STAMPS=1) */
 int vap_test_read_lnproj_stamps(unsigned long long* out);
-/* timing diagnostics: 8 x 32 s_memtime stamps of sampled row-panel workgroups (VAP_RP_STAMPS=1) */
-int vap_test_read_rp_stamps(unsigned long long* out);
-/* timing diagnostics (VAP_FFN_STAMPS=1): 8 x 24 s_memtime stamps of sampled fused-FFN workgroups, then
- * 1024 x 2 s_memrealtime start / end of every workgroup (out holds 2240 values) */
-int vap_test_read_ffn_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 2 x 4 x 6 s_memtime stamps of sampled bf16 GEMM k-steps (VAP_GEMM2_STAMPS=1) */
 int vap_test_read_gemm_stamps(unsigned long long* out);  /* + 8 x 6 tile-phase stamps after the 8 x 2 x 4 x 6 */
 /* CPC conv2..4 slab kernel (k_conv234.hip) on its own: conv k4 s2 256->256 + bias + ChannelNorm + ReLU.

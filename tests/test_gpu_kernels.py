@@ -249,71 +249,6 @@ def test_layernorm(prec):
     assert (raw.float().cpu() - x.to(dt).float()).abs().max().item() == 0
 
 
-@pytest.mark.parametrize("amode,epi,N", [(1, 0, 768), (1, 0, 256), (1, 1, 768), (2, 0, 512), (0, 2, 256)])
-@pytest.mark.parametrize("M", [1, 77, 1000])
-@pytest.mark.parametrize("packed", [0, 1])
-def test_rowpanel(amode, epi, N, M, packed):
-    """Row-panel projection GEMM (bf16 perf path): LN / raw fp32 / bf16 A panel, bf16 / GELU /
-    fp32+residual epilogue, ragged last panel; W in the plain or the packed row-panel layout."""
-    L = lib()
-    D = 256
-    g = torch.Generator().manual_seed(11 + M + N)
-    x = torch.randn(M, D, generator=g) * 2 + 0.5
-    ga = 1 + 0.2 * torch.randn(D, generator=g)
-    be = 0.1 * torch.randn(D, generator=g)
-    W = (torch.randn(N, D, generator=g) / 16).to(torch.bfloat16)
-    add = torch.randn(M, N, generator=g) if epi == 2 else None
-    A = x.to(torch.bfloat16) if amode == 0 else x
-    dA, dW, dga, dbe = A.cuda(), W.cuda(), ga.cuda(), be.cuda()
-    dadd = add.cuda() if add is not None else None
-    C = torch.zeros(M, N, device="cuda", dtype=torch.float32 if epi == 2 else torch.bfloat16)
-    if packed:  # [N/256][K/32][16 row groups][64 lanes][8]: lane = (k%32)/8*16 + n%16
-        dW = dW.view(N // 256, 16, 16, 8, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
-    _run(L.lib().vap_test_rowpanel, _p(dA), D, M, _p(dW), D, N, _p(C), N, _p(dadd),
-         _p(dga) if amode == 1 else None, _p(dbe) if amode == 1 else None, amode | (16 * packed), epi, _st())
-    a = F.layer_norm(x, (D,), ga, be) if amode == 1 else x
-    ref = a.to(torch.bfloat16).float() @ W.float().t()
-    if epi == 1:
-        ref = F.gelu(ref)
-    if epi == 2:
-        ref = ref + add
-    err = (C.float().cpu() - ref).abs().max().item()
-    tol = 1e-4 if epi == 2 else 2e-2  # fp32 output: accumulation order only; bf16 output rounding
-    assert err <= tol * max(1.0, ref.abs().max().item()), f"rowpanel({amode},{epi},{N}) M={M}: {err}"
-
-
-def test_rowpanel_rejects_bad_shapes():
-    L = lib()
-    z = torch.zeros(64, 256, device="cuda")
-    W = torch.zeros(200, 256, device="cuda", dtype=torch.bfloat16)
-    C = torch.zeros(64, 200, device="cuda", dtype=torch.bfloat16)
-    rc = L.lib().vap_test_rowpanel(_p(z), 256, 64, _p(W), 256, 200, _p(C), 200, None, None, None, 2, 0, _st())
-    assert rc != 0
-
-
-@pytest.mark.parametrize("M", [1, 77, 1000])
-def test_ffn_fused(M):
-    """Fused FFN block (bf16 path): x += W2 . GELU(W1 . LN(x)) with the hidden in LDS, against the
-    torch fp32 composition on the same bf16-rounded operands (the LN output and the GELU output are
-    rounded to bf16 inside the kernel, as the unfused row-panel path rounds them)."""
-    L = lib()
-    D = 256
-    g = torch.Generator().manual_seed(21 + M)
-    x = torch.randn(M, D, generator=g) * 2 + 0.3
-    ga = 1 + 0.2 * torch.randn(D, generator=g)
-    be = 0.1 * torch.randn(D, generator=g)
-    W1 = (torch.randn(3 * D, D, generator=g) / 16).to(torch.bfloat16)
-    W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16)
-    dx = x.clone().cuda()
-    d = [t.cuda() for t in (W1, W2, ga, be)]
-    _run(L.lib().vap_test_ffn, _p(dx), M, _p(d[0]), _p(d[1]), _p(d[2]), _p(d[3]), _st())
-    a = F.layer_norm(x, (D,), ga, be).to(torch.bfloat16).float()
-    hdn = F.gelu(a @ W1.float().t()).to(torch.bfloat16).float()
-    ref = x + hdn @ W2.float().t()
-    err = (dx.cpu() - ref).abs().max().item()
-    assert err <= 2e-3 * max(1.0, ref.abs().max().item()), f"ffn M={M}: {err}"
-
-
 @pytest.mark.parametrize("M,cus", [(1, 256), (77, 256), (1000, 256), (1000, 8), (5000, 16), (4700, 256)])
 @pytest.mark.parametrize("oproj", [True, False])
 def test_block_fused(M, cus, oproj):

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Kernel microbenchmarks through the test ABI (GPU box): isolated per-launch times of the
-transformer projection kernels at the bench's per-range shape (32 sequences x 1000 frames).
+transformer row kernels, the attention and the generic GEMM at the bench's shapes.
 
-    python tools/mb_kernels.py [--rows 32000] [--iters 50]
+    python tools/mb_kernels.py [--which rows,attn,gemm] [--rows 81920] [--iters 50]
 """
 import argparse
 import ctypes
@@ -116,118 +116,70 @@ def bench_gemm(lib, dev, st, iters, only=""):
     return res
 
 
-def bench_ffn(lib, dev, st, iters, M):
-    """Fused FFN block vs the unfused row-panel up + GEMM down, at one layer-chunk (M rows)."""
+def bench_rows(lib, dev, st, iters, M):
+    """The transformer row kernels (k_block.hip) at one layer-chunk of M rows: LN + QKV + raw cross
+    K/V, out-projection + LN + cross Q, LN + QKV, and the fused layer tail (out-proj + LN + FFN)."""
     g = torch.Generator(device="cpu").manual_seed(3)
     D = 256
-    x0 = torch.randn(M, D, generator=g).to(dev)
-    x = x0.clone()
+    x = torch.randn(M, D, generator=g).to(dev)
     ga = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
     be = (0.1 * torch.randn(D, generator=g)).to(dev)
-    W1 = (torch.randn(3 * D, D, generator=g) / 16).to(torch.bfloat16).to(dev)
-    W2 = (torch.randn(D, 3 * D, generator=g) / 28).to(torch.bfloat16).to(dev)
-    FF = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
 
-    W1p, W2p = torch.empty_like(W1), torch.empty_like(W2)
-    _native.check(lib.vap_test_pack_weight(ptr(W1), ptr(W1p), 3 * D, D, st))
-    _native.check(lib.vap_test_pack_weight(ptr(W2), ptr(W2p), D, 3 * D, st))
-
-    def fused():
-        _native.check(lib.vap_test_ffn_packed(ptr(x), M, ptr(W1p), ptr(W2p), ptr(ga), ptr(be), st))
-
-    def unfused():
-        _native.check(lib.vap_test_rowpanel(ptr(x), D, M, ptr(W1), D, 3 * D, ptr(FF), 3 * D, None, ptr(ga), ptr(be),
-                                            1, 1, st))
-        _native.check(lib.vap_test_gemm(1, ptr(FF), 3 * D, M * 3 * D, ptr(W2), 3 * D, D, None, M, 1, ptr(x), D, M * D,
-                                        ptr(x), D, M * D, None, None, 0, 0, 1, st))
-    Wo = (torch.randn(D, D, generator=g) / 16).to(torch.bfloat16).to(dev)
-    Wop = torch.empty_like(Wo)
-    _native.check(lib.vap_test_pack_weight(ptr(Wo), ptr(Wop), D, D, st))
+    def packed(n, k, scale):
+        W = (torch.randn(n, k, generator=g) * scale).to(torch.bfloat16).to(dev)
+        Wp = torch.empty_like(W)
+        _native.check(lib.vap_test_pack_weight(ptr(W), ptr(Wp), n, k, st))
+        return Wp
+    W1p, W2p, Wop = packed(3 * D, D, 1 / 16), packed(D, 3 * D, 1 / 28), packed(D, D, 1 / 16)
+    Wqkv, Wkv, Wq = packed(3 * D, D, 1 / 16), packed(2 * D, D, 1 / 16), packed(D, D, 1 / 16)
     O = torch.randn(M, D, generator=g).to(torch.bfloat16).to(dev)
-    cus = int(os.environ.get("MB_CUS", "248"))
+    cp = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+    cr = torch.empty(M, 2 * D, device=dev, dtype=torch.bfloat16)
+    cus = int(os.environ.get("MB_CUS", "0"))
 
-    def block():  # out-proj + residual + LN + FFN + residual in one launch
+    def block():
         _native.check(lib.vap_test_block_packed(ptr(x), ptr(O), M, ptr(Wop), ptr(W1p), ptr(W2p), ptr(ga), ptr(be),
                                                 cus, st))
 
-    def oproj_ffn():  # the pair it replaces: row-panel out-proj (+ residual) then the fused FFN
-        _native.check(lib.vap_test_rowpanel(ptr(O), D, M, ptr(Wop), D, D, ptr(x), D, ptr(x), None, None, 16, 2, st))
-        fused()
+    def qkv_kv():
+        _native.check(lib.vap_test_lnproj_packed(ptr(x), None, M, None, ptr(Wqkv), 3, ptr(Wkv), 2, ptr(cp), ptr(cr),
+                                                 ptr(ga), ptr(be), st))
 
+    def qkv():
+        _native.check(lib.vap_test_lnproj_packed(ptr(x), None, M, None, ptr(Wqkv), 3, None, 0, ptr(cp), None,
+                                                 ptr(ga), ptr(be), st))
+
+    def oproj_q():
+        _native.check(lib.vap_test_lnproj_packed(ptr(x), ptr(O), M, ptr(Wop), ptr(Wq), 1, None, 0, ptr(cp), None,
+                                                 ptr(ga), ptr(be), st))
     res = {}
-    for name, fn in [("ffn_fused", fused), ("ffn_unfused", unfused), ("oproj_ffn", oproj_ffn), ("block", block)]:
+    for name, fn, n_mac in [("block", block, D * D + 2 * 3 * D * D), ("lnproj_qkv_kv", qkv_kv, 5 * D * D),
+                            ("lnproj_qkv", qkv, 3 * D * D), ("lnproj_oproj_q", oproj_q, 2 * D * D)]:
         us = timeit(fn, iters)
-        res[name] = dict(us=round(us, 2), tflops=round(2.0 * M * 2 * 3 * D * D / us / 1e6, 1))
+        res[name] = dict(us=round(us, 2), tflops=round(2.0 * M * n_mac / us / 1e6, 1))
         print(name, res[name], flush=True)
     return res
 
 
-def pack_rowpanel(W):
-    """[N][256] bf16 -> the packed row-panel layout [N/256][8][16][64][8] (lane = (k%32)/8*16 + n%16)."""
-    N = W.shape[0]
-    return W.view(N // 256, 16, 16, 8, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", type=int, default=32000)
+    ap.add_argument("--rows", type=int, default=81920, help="rows of the row-kernel launches")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--which", default="rowpanel,attn")
+    ap.add_argument("--which", default="rows,attn")
     ap.add_argument("--case", default="", help="only GEMM cases whose name contains this")
-    ap.add_argument("--packed", action="store_true", help="row-panel W in the packed layout")
-    ap.add_argument("--attn-seqs", type=int, default=32, help="sequences of the attention benchmark")
+    ap.add_argument("--attn-seqs", type=int, default=128, help="sequences of the attention benchmark")
     ap.add_argument("--attn-frames", type=int, default=1000)
     args = ap.parse_args()
     lib = _native.lib()
     dev = torch.device("cuda:0")
-    M, D = args.rows, 256
-    g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(M, D, generator=g).to(dev)
-    xb = x.to(torch.bfloat16)
-    gamma = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
-    beta = (0.1 * torch.randn(D, generator=g)).to(dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
     if "attn" in args.which:
         res.update(bench_attn(lib, dev, st, args.iters, S=args.attn_seqs, T=args.attn_frames))
-    if "ffn" in args.which:
-        res.update(bench_ffn(lib, dev, st, args.iters, args.rows))
+    if "rows" in args.which:
+        res.update(bench_rows(lib, dev, st, args.iters, args.rows))
     if "gemm" in args.which:
         res.update(bench_gemm(lib, dev, st, args.iters, args.case))
-    if "rowpanel" not in args.which:
-        print(json.dumps(res))
-        return
-    for name, amode, epi, N in [("qkv_ln", 1, 0, 768), ("q_ln", 1, 0, 256), ("ff1_ln_gelu", 1, 1, 768),
-                                ("kv_raw", 2, 0, 512), ("proj_resid", 0, 2, 256)]:
-        W = (torch.randn(N, D, generator=g) / 16).to(dev).to(torch.bfloat16)
-        A = xb if amode == 0 else x
-        add = torch.randn(M, N, generator=g).to(dev) if epi == 2 else None
-        C = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == 2 else torch.bfloat16)
-
-        Wk = pack_rowpanel(W) if args.packed else W
-
-        def run():
-            _native.check(lib.vap_test_rowpanel(ptr(A), D, M, ptr(Wk), D, N, ptr(C), N, ptr(add),
-                                                ptr(gamma) if amode == 1 else None,
-                                                ptr(beta) if amode == 1 else None,
-                                                amode | (16 if args.packed else 0), epi, st))
-        us = timeit(run, args.iters)
-        # check against torch (fp32 math on the bf16-rounded operands)
-        a = x
-        if amode == 1:
-            a = torch.nn.functional.layer_norm(x, (D,), gamma, beta, 1e-5)
-        a = a.to(torch.bfloat16).float()
-        ref = a @ W.float().t()
-        if epi == 1:
-            ref = torch.nn.functional.gelu(ref)
-        if epi == 2:
-            ref = ref + add
-        err = (C.float() - ref).abs().max().item()
-        flops = 2.0 * M * N * D
-        byts = M * D * (2 if amode == 0 else 4) + M * N * (4 if epi == 2 else 2) + (M * N * 4 if epi == 2 else 0)
-        res[name] = dict(us=round(us, 2), tflops=round(flops / us / 1e6, 1), tbps=round(byts / us / 1e6, 2),
-                         max_err=round(err, 4))
-        print(name, res[name], flush=True)
     print(json.dumps(res))
 
 

@@ -32,14 +32,8 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros((8, 24), dtype=np.uint64)
     N.check(N.lib().vap_test_read_stamps(ctypes.c_void_p(buf.ctypes.data)))
-    if not any(os.environ.get(f"VAP_CONV01_V{v}") for v in (2, 4)):  # v9 / v10 (default)
-        # v11: start | waveform in LDS | split-sample rows | slices 0, 1 | units 0-7, 8-15, 16-23, 24-31 |
-        # epilogue (v9 / v10 have no waveform / split-sample stamps)
-        names, n = ["wv_load", "sv_build", "slices01", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 9
-    elif os.environ.get("VAP_CONV01_V4"):  # v4: start | prologue | units 0-7, 8-15, 16-23, 24-31 | epilogue
-        names, n = ["prologue", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 7
-    else:
-        names, n = ["prologue"] + [f"p{r}_{x}" for r in range(4) for x in ("sv", "g", "ksteps")] + ["epilogue"], 14
+    # start | waveform in LDS | split-sample rows | slices 0, 1 | units 0-7, 8-15, 16-23, 24-31 | epilogue
+    names, n = ["wv_load", "sv_build", "slices01", "u0_7", "u8_15", "u16_23", "u24_31", "epilogue"], 9
     for i in range(8):
         st = buf[i].astype(np.int64)
         d = np.diff(st[:n])

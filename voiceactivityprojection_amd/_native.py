@@ -80,8 +80,6 @@ _SIGS = {
     "vap_test_conv0": (ctypes.c_int, [ctypes.c_int, _P, ctypes.c_int, _I64, ctypes.c_int, _P, _P, _P, _P, _P, _P]),
     "vap_test_layernorm": (ctypes.c_int, [ctypes.c_int, _P, _I64, _P, _P, _P, _P, _P]),
     "vap_test_read_stamps": (ctypes.c_int, [_P]),
-    "vap_test_read_rp_stamps": (ctypes.c_int, [_P]),
-    "vap_test_read_ffn_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_block_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_lnproj_stamps": (ctypes.c_int, [_P]),
     "vap_test_read_gemm_stamps": (ctypes.c_int, [_P]),
@@ -89,14 +87,11 @@ _SIGS = {
     "vap_test_heads": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "vap_test_read_lstm_handoff": (ctypes.c_int, [_P]),
     "vap_test_read_lstm_xcc": (ctypes.c_int, [_P]),
-    "vap_test_ffn": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_pack_weight": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, _P]),
-    "vap_test_ffn_packed": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_block": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_int, _P]),
     "vap_test_lnproj": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
+    "vap_test_lnproj_packed": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, _P]),
     "vap_test_block_packed": (ctypes.c_int, [_P, _P, ctypes.c_int, _P, _P, _P, _P, _P, ctypes.c_int, _P]),
-    "vap_test_rowpanel": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P, _I64,
-                                         _P, _P, _P, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_probe_mfma_f32": (ctypes.c_int, [_P, _P, _P, _P]),
     "vap_test_convk4": (ctypes.c_int, [_P, _I64, ctypes.c_int, _P, _P, _P, _P, _P, _I64, ctypes.c_int, ctypes.c_int, _P]),
     "vap_test_convk4_stamps": (ctypes.c_int, [_P]),

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// bf16 perf-mode kernel: 128 queries per workgroup (4 waves x 32 = two 16-query MFMA column
+// bf16 perf-mode attention: 128 queries per workgroup (4 waves x 32 = two 16-query MFMA column
 // blocks per wave, sharing every K/V fragment read), K/V tiles of 64 keys double-buffered in LDS
 // (register prefetch of tile kb+1 while tile kb computes), V kept row-major and fed to the
 // O^T = V^T P^T MFMA through ds_read_b64_tr_b16 (hardware transpose read: no scalar transposed
@@ -174,153 +174,8 @@ VAP_DEV u32x2 tr_read(const unsigned char* p) {
   return __builtin_bit_cast(u32x2, v);
 }
 
-__global__ __launch_bounds__(256) void attn2_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char kv[2][2][KB2 * TROW];  // [buf][K,V]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
-  const int ks = a.kv_swap ? (s ^ 1) : s;
-  const bf16* Qs = (const bf16*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
-  const bf16* Ks = (const bf16*)a.K + (int64_t)ks * a.k_seq + h * HDIM;
-  const bf16* Vs = (const bf16*)a.V + (int64_t)ks * a.v_seq + h * HDIM;
-  constexpr float LOG2E = 1.4426950408889634f;
-  const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
-  const int qw0 = qb * QB2 + w * 32;  // first query of this wave
-  const int qlast = min(qb * QB2 + QB2 - 1, a.T - 1);
-  const int nkb = qlast / KB2 + 1;
-
-  chunk16 qf[2][2];
-  int qv[2];
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
-    qv[qs] = qw0 + qs * 16 + (lane & 15);
-    const int qc = qv[qs] < a.T ? qv[qs] : a.T - 1;
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg) qf[qs][kg] = *(const chunk16*)(Qs + (int64_t)qc * a.q_ld + (kg * 4 + (lane >> 4)) * 8);
-  }
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
-  f32x4 o[2][4];
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[qs][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // staging: K and V tiles are 512 chunks each; 2 + 2 per thread
-  chunk16 rk[2], rv[2];
-  auto gload = [&](int kb) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + i * 256, row = id >> 3, c = id & 7, key = kb * KB2 + row;
-      rk[i] = key < a.T ? *(const chunk16*)(Ks + (int64_t)key * a.k_ld + c * 8) : chunk16{0, 0, 0, 0};
-      rv[i] = key < a.T ? *(const chunk16*)(Vs + (int64_t)key * a.v_ld + c * 8) : chunk16{0, 0, 0, 0};
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + i * 256, row = id >> 3, c = id & 7;
-      *(chunk16*)(kv[buf][0] + row * TROW + kswz2(row, c) * 16) = rk[i];
-      *(chunk16*)(kv[buf][1] + row * TROW + c * 16) = rv[i];
-    }
-  };
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nkb) gload(kb + 1);
-    const int key0 = kb * KB2;
-    if (key0 <= qw0 + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
-      const unsigned char* Kt = kv[cur][0];
-      const unsigned char* Vt = kv[cur][1];
-      f32x4 st[2][4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const int row = kt * 16 + (lane & 15);
-        const chunk16 k0 = *(const chunk16*)(Kt + row * TROW + kswz2(row, lane >> 4) * 16);
-        const chunk16 k1 = *(const chunk16*)(Kt + row * TROW + kswz2(row, 4 + (lane >> 4)) * 16);
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs) {
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          acc = mfma_chunk<bf16>(k0, qf[qs][0], acc);
-          acc = mfma_chunk<bf16>(k1, qf[qs][1], acc);
-          st[qs][kt] = acc;
-        }
-      }
-      const bool diag = key0 + KB2 - 1 > qw0;  // some key of the tile lies above some query
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        float bm = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = key0 + kt * 16 + (lane >> 4) * 4 + r;
-            float v = fmaf(st[qs][kt][r], c2, sl2 * (float)(key - qv[qs]));
-            if (diag && key > qv[qs]) v = -INFINITY;
-            st[qs][kt][r] = v;
-            bm = fmaxf(bm, v);
-          }
-        bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-        const float mn = fmaxf(m[qs], bm);
-        const float alpha = __builtin_amdgcn_exp2f(m[qs] - mn);
-        m[qs] = mn;
-        float ps = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(st[qs][kt][r] - mn);
-            st[qs][kt][r] = pv;
-            ps += pv;
-          }
-        lsum[qs] = lsum[qs] * alpha + ps;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qs][dt] *= alpha;
-      }
-      // O^T[d][q] += V^T[d][key] P^T[key][q]; A = V^T via transpose reads of the row-major V tile:
-      // lane 4q'+p of a 16-lane group addresses key row kb0 + q', columns dt*16 + 4p .. + 3.
-      const int qq = (lane & 15) >> 2, pp = lane & 3;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 pb[2];
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs)
-          pb[qs] = bf16x8{(bf16)st[qs][2 * kk][0], (bf16)st[qs][2 * kk][1], (bf16)st[qs][2 * kk][2],
-                          (bf16)st[qs][2 * kk][3], (bf16)st[qs][2 * kk + 1][0], (bf16)st[qs][2 * kk + 1][1],
-                          (bf16)st[qs][2 * kk + 1][2], (bf16)st[qs][2 * kk + 1][3]};
-        const int r0 = 32 * kk + (lane >> 4) * 4 + qq;  // keys of the first 4-key block (+16 for the second)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const u32x2 v0 = tr_read(Vt + r0 * TROW + (dt * 16 + 4 * pp) * 2);
-          const u32x2 v1 = tr_read(Vt + (r0 + 16) * TROW + (dt * 16 + 4 * pp) * 2);
-          const chunk16 af = {v0.x, v0.y, v1.x, v1.y};
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs) o[qs][dt] = mfma_chunk<bf16>(af, __builtin_bit_cast(chunk16, pb[qs]), o[qs][dt]);
-        }
-      }
-    }
-    if (kb + 1 < nkb) lstore(cur ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
-    float lt = lsum[qs] + __shfl_xor(lsum[qs], 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
-    const float inv = 1.0f / lt;
-    if (qv[qs] < a.T) {
-      bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv[qs] * a.o_ld + h * HDIM;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + (lane >> 4) * 4;
-        store4(orow + d, o[qs][dt][0] * inv, o[qs][dt][1] * inv, o[qs][dt][2] * inv, o[qs][dt][3] * inv);
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------
-// attn3: attn2's tiling with the softmax VALU cut down (the kernel is VALU-bound at head_dim 64:
+// attn3: that tiling with the softmax VALU cut down (the kernel is VALU-bound at head_dim 64:
 // ~256 MFMA FLOPs but ~6 VALU ops per score):
 //  * the query term of the AliBi bias cancels in the softmax, so v = s*c2 + sl2*key: one FMA per
 //    score against a per-tile key-bias vector (16 registers, one add per 2 scores per tile);
@@ -524,19 +379,10 @@ template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.T <= 0 || a.S <= 0 || a.H <= 0) return hipErrorInvalidValue;
   if constexpr (sizeof(T) == 2) {
-    static const int ver = getenv("VAP_ATTN_V1") ? 1 : getenv("VAP_ATTN_V2") ? 2 : 3;
     if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
-    if (ver == 3) {
-      const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
-      hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
-      return hipGetLastError();
-    }
-    if (a.q0 != 0) return hipErrorInvalidValue;
-    if (ver == 2) {
-      dim3 grid((a.T + QB2 - 1) / QB2, a.H, a.S);
-      hipLaunchKernelGGL(attn2_kernel, grid, dim3(256), 0, st, a);
-      return hipGetLastError();
-    }
+    const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
+    hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
+    return hipGetLastError();
   }
   if (a.q0 != 0) return hipErrorInvalidValue;
   dim3 grid((a.T + QB - 1) / QB, a.H, a.S);

@@ -5,13 +5,11 @@
 //
 // The conv0 activation (256 ch x 64000 positions per speaker per 20 s: 4.2 GB bf16 at batch 64) is
 // never written to HBM.  conv1 (k=8, s=4, p=2) output t reads conv0 positions 4t-2+j, j = 0..7.
-// Split j = r + 4h (phase r = 0..3, half h = 0..1): for a tile of 128 outputs [t0, t0+128) and a
-// phase r, the needed positions are G_r[i] = x0[4(t0+i) - 2 + r], i = 0..128, and output row i uses
-// G_r[i] (h = 0) and G_r[i+1] (h = 1).  Per phase the workgroup regenerates G_r (129 x 256 bf16) in
-// LDS and runs the 512-deep K slice (taps r and r+4) of the conv1 GEMM against W1 tiles streamed
-// from L2.  Every conv0 position is generated once per tile (plus one halo row per phase).  That is
-// the v2 kernel below (VAP_CONV01_V2=1); the default v9 kernel makes the same image in 32-channel
-// slices inside the MFMA stream on 256-row tiles (see its header).
+// Split j = r + 4h (phase r = 0..3, half h = 0..1): for a tile of outputs [t0, t0+256) and a phase
+// r, the needed positions are G_r[i] = x0[4(t0+i) - 2 + r], i = 0..256, and output row i uses G_r[i]
+// (h = 0) and G_r[i+1] (h = 1).  The kernel makes G_r in 32-channel SLICES inside the conv1 MFMA
+// stream (see conv01m_kernel's header); every conv0 position is generated once per tile (plus one
+// halo row per phase).
 //
 // conv0 itself runs on the MFMA: z^T[c][p] = sum_k A[c][k] S[k][p] with a K = 32 split-bf16 layout
 //   k  0..9 : A = w_hi[c],  S = s_hi[p]      k 10..19: A = w_hi[c], S = s_lo[p]
@@ -21,6 +19,9 @@
 // rstd_p comes from the exact centred quadratic form  var = (s^T G s + 2 h.s + beta)/255,
 // G = Wc^T Wc (10x10), h = Wc^T bc, beta = bc.bc  (Wc, bc = centred conv0 weights / bias), so the
 // statistics need no pass over the 256 channels.  Padding positions (p < 0 or p >= L0) are zero rows.
+//
+// Earlier generations (whole-phase G images v2, four-wave slices v9, 16x16x32 MFMAs v10) were
+// retired in round 3; DESIGN.md section 3.1 keeps their measurements.
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
@@ -30,24 +31,6 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 256, GROWS = BM + 1, GROWB = 512;  // G image: 129 rows x 256 ch bf16
-constexpr int NPOS = 144;                                      // 9 position tiles of 16 (>= 129)
-constexpr int SVROW = 80;                                      // padded split-sample row (32 bf16 + pad)
-constexpr int BROWB = 128;                                     // W1 staging row: 64 k bf16
-constexpr int OFF_G = 0;
-constexpr int OFF_B = OFF_G + GROWS * GROWB;      // 66048
-constexpr int OFF_SV = OFF_B + 2 * BN * BROWB;    // + 65536
-constexpr int OFF_RS = OFF_SV + NPOS * SVROW;     // + 11520
-constexpr int LDS_BYTES = OFF_RS + NPOS * 4;      // + 576 = 143680
-
-VAP_DEV int gswz(int row, int c16) { return c16 ^ (row & 15); }      // 32 chunks per G row
-// v2 G layout: chunk c of row r at position (c&1)*16 + ((c>>1) ^ r)&15 of the 512-B row -- chunks c and
-// c+1 share a bank slot in opposite 256-B halves, so the slot depends on the row only and the
-// fragment reads stay conflict-free for both tap offsets (rows m and m+1); the XOR of gswz is
-// 2-way conflicted on the shifted rows.
-VAP_DEV int gpos(int row, int c16) { return (c16 & 1) * 16 + (((c16 >> 1) ^ row) & 15); }
-VAP_DEV int bswz(int row, int c) { return c ^ ((row >> 1) & 7); }    // 8 chunks per W1 staging row
-
 struct C0Stat {  // layout of the c0stat float array (host-computed at weight packing)
   static constexpr int G = 0;     // 10x10 centred Gram matrix
   static constexpr int H = 100;   // 10
@@ -55,295 +38,10 @@ struct C0Stat {  // layout of the c0stat float array (host-computed at weight pa
   static constexpr int N = 112;
 };
 
-// ------------------------------------------------------------------------------------------
-// v2 (VAP_CONV01_V2=1): the same fused math, restaged for the MI355X memory pipeline:
-//   * W1 k-tiles (256 rows x 64 k) arrive by LDS-DMA (global_load_lds_dwordx4, swizzle applied to
-//     the source address), two stages, raw s_barrier + vmcnt: the next tile's DMA stays in flight
-//     across the MFMAs, the phase barriers and the conv0 regeneration;
-//   * the tile's whole waveform segment (~10 KiB, every phase's samples) is loaded into LDS once, so
-//     a phase's split samples / ChannelNorm statistics come from LDS instead of dependent global loads;
-//   * operands swapped (C^T = W1 G^T): a lane owns 4 consecutive output channels of one row ->
-//     8-byte bf16 stores (16 per lane instead of 64 two-byte stores), ChannelNorm row statistics by a
-//     16-lane-stride shuffle + LDS.
-// ------------------------------------------------------------------------------------------
-constexpr int WSEG = 2592;                           // waveform floats per tile: 20*128 + 15 + 10 (+pad)
-constexpr int B_OFF_G = 0;
-constexpr int B_OFF_W = B_OFF_G + GROWS * GROWB;     // 66048: 2 W1 stages of 256 x 128 B
-constexpr int B_OFF_SV = B_OFF_W + 2 * BN * BROWB;   // + 65536
-constexpr int B_OFF_RS = B_OFF_SV + NPOS * SVROW;    // + 11520
-constexpr int B_OFF_WV = B_OFF_RS + NPOS * 4;        // + 576
-constexpr int B_LDS = B_OFF_WV + WSEG * 4;           // + 10368 = 154048
-typedef __attribute__((address_space(3))) void lds_void_t;
-constexpr int WST = BN * 64;                          // v2 W1 stage: 256 rows x 64 B (4 stages = B_OFF_W area)
-VAP_DEV int wswz(int row, int c) { return c ^ ((row >> 2) & 2); }  // 64-B rows: conflict-free b128 reads
-
-VAP_DEV void lds_barrier() {  // LDS writes retired + workgroup barrier, without draining the DMA
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // timing diagnostics (VAP_CONV01_STAMPS=1): s_memtime at the phase boundaries of sampled
 // workgroups, read back with vap_test_read_stamps(); the production instantiation records nothing
 __device__ unsigned long long g_conv01_stamps[8][24];
 
-template <bool STAMPS>
-__global__ __launch_bounds__(512, 1) void conv01b_kernel(const float* __restrict__ wav, int64_t N, int L0,
-                                                        const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
-                                                        const float* __restrict__ beta0, const bf16* __restrict__ W1,
-                                                        const float* __restrict__ b1, const float* __restrict__ g1,
-                                                        const float* __restrict__ be1, bf16* __restrict__ out,
-                                                        int64_t out_seq_stride, int r0, int r1) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[B_LDS];
-  unsigned char* G = smem + B_OFF_G;
-  unsigned char* Wt = smem + B_OFF_W;
-  unsigned char* SV = smem + B_OFF_SV;
-  float* RS = (float*)(smem + B_OFF_RS);
-  float* WV = (float*)(smem + B_OFF_WV);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1;  // 64 rows (t) x 64 output channels per wave
-  const int s = blockIdx.y;
-  const int t0 = r0 + blockIdx.x * BM;
-  const float* src = wav + (int64_t)s * N;
-  const unsigned char* W1b = (const unsigned char*)W1;
-  // conv0 operand fragments of this wave (channel tiles 2w, 2w+1) and folded ChannelNorm shifts
-  chunk16 a0f[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) a0f[j] = c0w[((2 * w + j) * 16 + (lane & 15)) * 4 + (lane >> 4)];
-  float bet[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bet[j][e] = beta0[(2 * w + j) * 16 + 4 * (lane >> 4) + e];
-  // sampled workgroups: block x in {0, 7}, sequence in {0, 1, 2, 3}
-  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 7) && s < 4) ? (s * 2 + (blockIdx.x == 7)) : -1;
-  unsigned long long stv[24];
-  int nst = 0;
-  auto stamp = [&]() {
-    if constexpr (STAMPS) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (nst < 24) stv[nst] = __builtin_amdgcn_s_memtime();
-      ++nst;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  stamp();
-
-  // W1 DMA, 4 stages of 256 rows x 64 B (k 32 deep): a piece = 16 rows x 64 B; wave w fills pieces
-  // 2w, 2w+1 of a 16-piece stage; lane -> (row 16p + lane/4, physical chunk lane%4) holding logical
-  // chunk (lane%4) ^ wswz(row).  Three stages stay in flight (counted vmcnt).
-  uint32_t woff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (w * 2 + i) * 16 + (lane >> 2);
-    woff[i] = (uint32_t)(row * 64 + wswz(row, lane & 3) * 16);
-  }
-  // W1 in the k-step-major layout [K/32][256][32] (launch_pack_kstep): one stage = 16 KiB contiguous
-  auto kstep_of = [](int q) {  // k-step q (0..63): phase q>>4, tap half (q>>3)&1, 32-channel group q&7
-    return ((q >> 4) + 4 * ((q >> 3) & 1)) * 8 + (q & 7);
-  };
-  auto dma = [&](int q) {
-    unsigned char* base = Wt + (q & 3) * WST;
-    const uint32_t kb = (uint32_t)kstep_of(q) * 16384;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(W1b + (woff[i] + kb)), (lds_void_t*)(base + (w * 2 + i) * 1024), 16, 0, 0);
-  };
-
-
-  // the tile's waveform segment: samples 20*t0 - 13 + [0, WSEG) (zeros outside the signal)
-  const int64_t xb = (int64_t)20 * t0 - 13;
-  for (int i = tid; i < WSEG; i += 512) {
-    const int64_t ix = xb + i;
-    WV[i] = (ix >= 0 && ix < N) ? src[ix] : 0.f;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only the DMA ring uses vmcnt from here on
-  dma(0);
-  dma(1);
-  dma(2);
-  lds_barrier();
-  stamp();
-
-  f32x4 acc[4][4];  // [n tile][m tile] of C^T
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int r = 0; r < 4; ++r) {
-    // ---------------- (a) split samples + ChannelNorm statistics of the phase positions (LDS only)
-    if (tid < NPOS) {
-      const int i = tid;
-      const int p = 4 * (t0 + i) - 2 + r;
-      const bool valid = i < GROWS && p >= 0 && p < L0;
-      float sm[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG - 1)];
-      bf16 hi[10], lo[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        hi[k] = (bf16)sm[k];
-        lo[k] = (bf16)(sm[k] - (float)hi[k]);
-      }
-      bf16x8 v0 = {hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]};
-      bf16x8 v1 = {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]};
-      bf16x8 v2 = {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]};
-      bf16x8 v3 = {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], (bf16)1.0f, (bf16)1.0f};
-      unsigned char* row = SV + i * SVROW;
-      *(bf16x8*)(row + 0) = v0;
-      *(bf16x8*)(row + 16) = v1;
-      *(bf16x8*)(row + 32) = v2;
-      *(bf16x8*)(row + 48) = v3;
-      float q = c0stat[C0Stat::BETA];
-#pragma unroll
-      for (int a = 0; a < 10; ++a) {
-        float ga = 2.0f * c0stat[C0Stat::H + a];
-#pragma unroll
-        for (int b = 0; b < 10; ++b) ga = fmaf(c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
-        q = fmaf(ga, sm[a], q);
-      }
-      RS[i] = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : -1.0f;
-    }
-    lds_barrier();  // SV/RS ready; every wave done reading the previous phase's G
-    stamp();
-
-    // ---------------- (b) conv0 on the MFMA -> ChannelNorm/ReLU -> bf16 G image
-#pragma unroll
-    for (int pt = 0; pt < NPOS / 16; ++pt) {
-      const int prow = pt * 16 + (lane & 15);
-      const chunk16 bfr = *(const chunk16*)(SV + prow * SVROW + (lane >> 4) * 16);
-      const float rs = RS[prow];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        z = mfma_chunk<bf16>(a0f[j], bfr, z);
-        if (prow < GROWS) {
-          const int c = (2 * w + j) * 16 + 4 * (lane >> 4);
-          bf16x4 o4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o4[e] = (bf16)(rs < 0.f ? 0.f : fmaxf(fmaf(rs, z[e], bet[j][e]), 0.f));
-          *(bf16x4*)(G + prow * GROWB + gpos(prow, c >> 3) * 16 + (c & 7) * 2) = o4;
-        }
-      }
-    }
-    lds_barrier();  // G ready
-    stamp();
-
-    // ---------------- (c) 16 k-steps of 32 over taps r (h = 0) and r + 4 (h = 1)
-    for (int kq = 0; kq < 16; ++kq) {
-      const int q = r * 16 + kq;
-      __builtin_amdgcn_sched_barrier(0);
-      // this wave's DMA of stage q landed: newer are stages q+1, q+2 (2 DMAs each, if issued)
-      if (q + 2 < 64) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (q + 1 < 64) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's stage q landed; stage q-1's buffer fully read
-      __builtin_amdgcn_sched_barrier(0);
-      if (q + 3 < 64) dma(q + 3);   // into stage q-1's buffer
-      const int hh = kq >> 3, kc = kq & 7;
-      const unsigned char* wb = Wt + (q & 3) * WST;
-      chunk16 gf[4], wf[4];
-      const int c16 = kc * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + (lane & 15) + hh;
-        gf[i] = *(const chunk16*)(G + row * GROWB + gpos(row, c16) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + (lane & 15);
-        wf[j] = *(const chunk16*)(wb + row * 64 + wswz(row, lane >> 4) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = mfma_chunk<bf16>(wf[j], gf[i], acc[j][i]);
-    }
-    stamp();
-  }
-
-  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[m = wm*64 + i*16 + lane%16][n = wn*64 + j*16 + (lane/16)*4 + e]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // no DMA in flight; every wave done with the W1 stages (reused below)
-  const int nb = wn * 64 + (lane >> 4) * 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x4 b = *(const f32x4*)(b1 + nb + j * 16);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] += b;
-  }
-  float* red = (float*)Wt;  // [BM][4 waves along N]
-  float mean[4], rstd[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float sum = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) sum += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    if ((lane >> 4) == 0) red[(wm * 64 + i * 16 + (lane & 15)) * 4 + wn] = sum;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane & 15)) * 4);
-    mean[i] = (pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / BN);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = acc[j][i][e] - mean[i];
-        ss += d * d;
-      }
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if ((lane >> 4) == 0) red[(wm * 64 + i * 16 + (lane & 15)) * 4 + wn] = ss;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (wm * 64 + i * 16 + (lane & 15)) * 4);
-    rstd[i] = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
-  }
-  bf16* obase = out + (int64_t)s * out_seq_stride;
-  // rows outer, column tiles inner: a wave completes each 128-B line of a row in consecutive stores
-  // (column-outer order wrote ~1.9x the output bytes to HBM: partial lines left L2 between stores)
-  f32x4 ga[4], be[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ga[j] = *(const f32x4*)(g1 + nb + j * 16);
-    be[j] = *(const f32x4*)(be1 + nb + j * 16);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int t = t0 + wm * 64 + i * 16 + (lane & 15);
-    if (t >= r1) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f32x4 v = (acc[j][i] - mean[i]) * rstd[i] * ga[j] + be[j];
-      store4(obase + (int64_t)t * BN + nb + j * 16, fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f),
-             fmaxf(v[3], 0.f));
-    }
-  }
-  if constexpr (STAMPS) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
-    if (samp >= 0 && tid == 0)
-      for (int k = 0; k < 24 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Shared pieces of the slice-pipelined kernel (v9)
-// ------------------------------------------------------------------------------------------
 VAP_DEV int sphys(int row, int c) { return (c + 2 * (row >> 2)) & 3; }  // 64-B slice / SV rows
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
@@ -353,383 +51,37 @@ VAP_DEV uint32_t relu_bf16x2(float a, float b) {  // bf16(max(x, 0)) for two val
   v = __builtin_elementwise_max(v, (s16x2){0, 0});
   return __builtin_bit_cast(uint32_t, v);
 }
-VAP_DEV void mfma_acc(f32x4& c, const chunk16& a, const chunk16& b) {
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-constexpr int BM2 = 256, NPOS2 = 272, GROWS2 = BM2 + 1;        // 17 position tiles of 16 (>= 257)
+constexpr int BM2 = 256, BN = 256, NPOS2 = 272, GROWS2 = BM2 + 1;  // 17 position tiles of 16 (>= 257)
 constexpr int WSEG2 = 20 * BM2 + 32;                            // 5152 waveform floats per tile
 constexpr int I_SVN = 4 * NPOS2;                                // 1088 split-sample rows
 constexpr int I_GSLOT = NPOS2 * 64;                             // 17408
 
 // ------------------------------------------------------------------------------------------
-// v9 (default): the conv0 image in (phase, 32-channel) SLICES on 256-row tiles, four waves.
+// conv01m_kernel: the conv0 image in (phase, 32-channel) SLICES on 256-row tiles, eight waves.
 // conv1's K for phase r is taps r and r+4 over 256 channels.  Ordered as units u = (r = u>>3,
 // g = u&7) of one 32-channel group with both taps (two 32-deep k-steps), a unit needs only the slice
 // G_r[:, 32g..+32) (257 rows x 64 B).  ChannelNorm-0 statistics are per position and closed-form,
 // so a slice is independent of the other channels and is made two units ahead, inside the MFMA
-// stream, instead of regenerating a whole-phase image between k-loops (v2: 27 % of a tile).
-//   * a wave owns 256 rows x 64 output channels: 64 MFMAs per k-step on 16 G + 4 W1 fragments, the
-//     256 accumulators in AGPRs (inline-asm MFMA with "+a"); no two waves share a W1 fragment, so
-//     W1 goes straight from L2 into VGPRs (k-step-major layout: one fragment = 1 KiB contiguous) --
-//     at 256 rows per tile the W1 stream is 16 B / cycle / CU, within what L2 sustains;
+// stream, instead of regenerating a whole-phase image between k-loops.
+//   * wave w owns output channels 32w .. 32w+31 for all 256 rows (8 row tiles of the 32x32x16
+//     MFMA, 128 accumulators in AGPRs through inline-asm "+a" MFMAs, so two waves share a SIMD and
+//     the partner's MFMAs fill the gaps one wave leaves);
+//   * W1 fragments are unique per wave and go straight from L2 into a two-set register ring one
+//     unit ahead (k-step-major layout: one fragment = 1 KiB contiguous);
 //   * ChannelNorm-0 folded into the conv0 operand: the prologue stores rstd_p * [s_hi | s_lo | s_hi |
 //     1 1] (split-bf16 after scaling) and the conv0 MFMA starts from beta0, so a slice is
 //     relu(MFMA) -> bf16 (v_pk_max_i16 on the packed bit patterns) with no per-position loads;
 //   * three slice slots (slice v in slot v%3): slice u+2 is made during unit u into the slot of
-//     slice u-1, so ONE barrier at the start of unit u publishes slice u+1 and frees that slot, and
-//     the G fragments are read just in time (3 MFMA groups ahead through a 4-register ring) instead
-//     of a whole k-step ahead -- which frees the VGPRs for
-//   * a three-set W1 register ring: unit u+2's fragments load at the start of unit u (64 KiB in
-//     flight per CU, two units of latency budget);
-//   * the slice work has no branches: every wave makes position tile 16 (the rows 256.. that only
-//     output row 255 reads), padding positions are zeroed with a per-lane validity mask, and slices
-//     past the last unit go to slots nothing reads.
+//     slice u-1, so ONE barrier at the start of unit u publishes slice u+1 and frees that slot;
+//   * slice work split by (channel tile ct = w & 1, position tiles w/2 + 4x; waves 0 and 1 also
+//     make tile 16, the rows 256.. only output row 255 reads); padding positions are zeroed with a
+//     per-lane validity mask;
+//   * G slots use the swizzle chunk' = (chunk + row/4) mod 4: conflict-free ds_read_b128 for 32
+//     consecutive rows (either tap offset) and for the slice stores of 16 rows;
+//   * epilogue rows are one lane each (row = lane % 32 of a row tile, 16 channels per lane, the
+//     other 16 in lane ^ 32): ChannelNorm-1 by one exchange of per-wave (mean, M2) pairs, 16-B
+//     stores via v_permlane32_swap.
 // The waveform segment (prologue only) shares its LDS with slot 2 and the epilogue's reduction area.
-// Stamps (VAP_CONV01_STAMPS, tools/stamps_conv01.py; 256-row tile): prologue 17k, 32 units 108k
-// (3.4k per unit against 2,048 cycles of MFMA: +0.4k W1 loads, +1k slice work), epilogue 22k.
-// ------------------------------------------------------------------------------------------
-constexpr int J_OFF_G = 0;                                    // 3 slots of 272 x 64 B
-constexpr int J_OFF_RED = J_OFF_G + 3 * I_GSLOT;              // 52224 (epilogue)
-constexpr int J_OFF_WV = J_OFF_G + 2 * I_GSLOT;               // 34816: over slot 2 + red (prologue)
-constexpr int J_OFF_SV = J_OFF_RED + BM2 * 4 * 4;             // 56320
-constexpr int J_OFF_C0 = J_OFF_SV + I_SVN * 64;               // 125952
-constexpr int J_OFF_BE = J_OFF_C0 + 256 * 64;                 // 142336
-constexpr int J_LDS = J_OFF_BE + 4 * 256 * 4;                 // 146432
-static_assert(J_OFF_WV + WSEG2 * 4 <= J_OFF_SV, "conv01 v9 waveform alias");
-static_assert(J_LDS <= 163840, "conv01 v9 LDS");
-
-template <bool STAMPS, int DIAG = 0>
-__global__ __launch_bounds__(256, 1) void conv01i_kernel(const float* __restrict__ wav, int64_t N, int L0,
-                                                        const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
-                                                        const float* __restrict__ beta0, const bf16* __restrict__ W1,
-                                                        const float* __restrict__ b1, const float* __restrict__ g1,
-                                                        const float* __restrict__ be1, bf16* __restrict__ out,
-                                                        int64_t out_seq_stride, int r0, int r1) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[J_LDS];
-  unsigned char* G = smem + J_OFF_G;
-  unsigned char* SV = smem + J_OFF_SV;
-  unsigned char* C0 = smem + J_OFF_C0;
-  float* BE = (float*)(smem + J_OFF_BE);
-  float* EP = BE + 256;
-  float* WV = (float*)(smem + J_OFF_WV);
-  float* red = (float*)(smem + J_OFF_RED);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 64w..64w+63, all 256 rows
-  const int s = blockIdx.y;
-  const int t0 = r0 + blockIdx.x * BM2;
-
-  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
-  unsigned long long stv[24];
-  int nst = 0;
-  auto stamp = [&]() {
-    if constexpr (STAMPS) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (nst < 24) stv[nst] = __builtin_amdgcn_s_memtime();
-      ++nst;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  stamp();
-
-  // W1 fragments by buffer loads: one lane offset VGPR, the k-step / fragment offset in an SGPR
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W1, 64 * 256 * 64);
-  const uint32_t wlo = (uint32_t)(((w * 64 + (lane & 15)) * 4 + (lane >> 4)) * 16);
-  auto wload = [&](int u, chunk16* wf) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kk = ((u >> 3) + 4 * h) * 8 + (u & 7);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wf[h * 4 + j] = buf_load16(wrs, wlo, (uint32_t)(kk * 16384 + j * 1024));
-    }
-  };
-
-  // ---------------- prologue
-  {
-    const __amdgpu_buffer_rsrc_t wr = make_rsrc(wav + (int64_t)s * N, (uint32_t)(N * 4));
-    const int xb = 20 * t0 - 13;  // first sample of the segment (negative offsets read as zero)
-    uint32_t wv[21];
-#pragma unroll
-    for (int k = 0; k < 21; ++k)
-      wv[k] = __builtin_amdgcn_raw_buffer_load_b32(wr, (int)((uint32_t)(xb + tid + 256 * k) * 4u), 0, 0);
-    chunk16 c0[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c0[i] = c0w[tid + i * 256];
-    f32x4 ep;
-    if (tid < 64) ep = ((const f32x4*)beta0)[tid];
-    else if (tid < 128) ep = ((const f32x4*)b1)[tid - 64];
-    else if (tid < 192) ep = ((const f32x4*)g1)[tid - 128];
-    else ep = ((const f32x4*)be1)[tid - 192];
-#pragma unroll
-    for (int k = 0; k < 21; ++k)
-      if (tid + 256 * k < WSEG2) WV[tid + 256 * k] = __builtin_bit_cast(float, wv[k]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ((chunk16*)C0)[tid + i * 256] = c0[i];
-    ((f32x4*)BE)[tid] = ep;
-  }
-  chunk16 W[3][8];  // W1 register ring: unit u in set u % 3
-  wload(0, W[0]);
-  wload(1, W[1]);
-  __syncthreads();
-
-  for (int j = tid; j < I_SVN; j += 256) {
-    const int r = j / NPOS2, i = j - r * NPOS2;
-    const int p = 4 * (t0 + i) - 2 + r;
-    const bool valid = i < GROWS2 && p >= 0 && p < L0;
-    float sm[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG2 - 1)];
-    float q = c0stat[C0Stat::BETA];
-#pragma unroll
-    for (int a = 0; a < 10; ++a) {
-      float ga = fmaf(c0stat[C0Stat::G + a * 10 + a], sm[a], 2.0f * c0stat[C0Stat::H + a]);
-#pragma unroll
-      for (int b = a + 1; b < 10; ++b) ga = fmaf(2.0f * c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
-      q = fmaf(ga, sm[a], q);
-    }
-    const float rs = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : 0.f;
-    bf16 hi[10], lo[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const float x = rs * sm[k];
-      hi[k] = (bf16)x;
-      lo[k] = (bf16)(x - (float)hi[k]);
-    }
-    const bf16 rb = (bf16)rs;
-    const bf16x8 v[4] = {{hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]},
-                         {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]},
-                         {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]},
-                         {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], rb, rb}};
-    unsigned char* row = SV + j * 64;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) *(bf16x8*)(row + sphys(j, c) * 16) = v[c];
-  }
-
-  // validity of this lane's position in tile x (w, w+4, w+8, w+12, 16) of phase r: bit 5r + x
-  uint32_t vmask = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int x = 0; x < 5; ++x) {
-      const int pt = x == 4 ? 16 : w + 4 * x;
-      const int p = 4 * (t0 + pt * 16 + (lane & 15)) - 2 + r;
-      vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
-    }
-  __syncthreads();
-
-  // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; rows >= 257 are never read
-  auto read_c0 = [&](int v, chunk16* c0, f32x4* bt) {
-    const int g = v & 7;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      c0[ct] = ((const chunk16*)C0)[((2 * g + ct) * 16 + (lane & 15)) * 4 + (lane >> 4)];
-      bt[ct] = *(const f32x4*)(BE + (2 * g + ct) * 16 + 4 * (lane >> 4));
-    }
-  };
-  auto read_sv = [&](int v, int x) -> chunk16 {
-    const int pt = x == 4 ? 16 : w + 4 * x;
-    const int jj = ((v >> 3) & 3) * NPOS2 + pt * 16 + (lane & 15);
-    return *(const chunk16*)(SV + jj * 64 + sphys(jj, lane >> 4) * 16);
-  };
-  auto pstore = [&](int v, int x, const f32x4* z) {
-    const int pt = x == 4 ? 16 : w + 4 * x;
-    const int prow = pt * 16 + (lane & 15);
-    const uint32_t m = 0u - ((vmask >> (5 * ((v >> 3) & 3) + x)) & 1u);
-    unsigned char* gs = G + (v % 3) * I_GSLOT;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const u32x2 o = {relu_bf16x2(z[ct][0], z[ct][1]) & m, relu_bf16x2(z[ct][2], z[ct][3]) & m};
-      const int lc = 2 * ct + (lane >> 5);
-      if constexpr (DIAG & 16) asm volatile("" ::"v"(o));
-      else *(u32x2*)(gs + prow * 64 + sphys(prow, lc) * 16 + ((lane >> 4) & 1) * 8) = o;
-    }
-  };
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {  // slices 0 and 1
-    chunk16 c0[2];
-    f32x4 bt[2], z[2];
-    read_c0(v, c0, bt);
-#pragma unroll
-    for (int x = 0; x < 5; ++x) {
-      const chunk16 sv = read_sv(v, x);
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) z[ct] = mfma_chunk<bf16>(c0[ct], sv, bt[ct]);
-      pstore(v, x, z);
-    }
-  }
-
-  f32x4 acc[4][16];  // [n tile][m tile] of C^T, in AGPRs
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment stream of unit u: n = 16h + i -> k-step (u,h), row block i; reads run 3 groups ahead
-  auto gread = [&](int u, int n) -> chunk16 {
-    const unsigned char* gs = G + (u % 3) * I_GSLOT;
-    const int row = (n & 15) * 16 + (lane & 15) + (n >> 4);
-    return *(const chunk16*)(gs + row * 64 + sphys(row, lane >> 4) * 16);
-  };
-  chunk16 gf[4];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // slices 0, 1 published; WV (slot 2) free
-#pragma unroll
-  for (int n = 0; n < 3; ++n) gf[n] = gread(0, n);
-  stamp();
-
-  auto unit = [&](const int u, chunk16* wf, chunk16* wn2, const bool last1, const bool last2) {
-    // B_u: own slice u+1 stores retired; W1 of unit u landed (unit u+1's 8 loads are younger)
-    __builtin_amdgcn_sched_barrier(0);
-    if (last1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!(DIAG & 4))
-      if (!last2) wload(u + 2, wn2);
-    const int v = u + 2;
-    chunk16 c0[2], sv;
-    f32x4 bt[2], z[2][2];
-    if constexpr (!(DIAG & 2)) read_c0(v, c0, bt);
-#pragma unroll
-    for (int n = 0; n < 32; ++n) {
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) {  // slice v: tile x operands at group 6x, MFMAs at 6x+2, stores at 6x+4
-        if (n % 6 == 0 && n / 6 < 5) {
-          if constexpr (DIAG & 64) sv = c0[0];
-          else sv = read_sv(v, n / 6);
-        }
-        if (n % 6 == 2 && n / 6 < 5)
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            if constexpr (DIAG & 32) z[(n / 6) & 1][ct] = bt[ct] + __builtin_bit_cast(f32x4, sv);
-            else z[(n / 6) & 1][ct] = mfma_chunk<bf16>(c0[ct], sv, bt[ct]);
-          }
-        if (n % 6 == 4 && n / 6 < 5) pstore(v, n / 6, z[(n / 6) & 1]);
-      }
-      const int i = n & 15, h = n >> 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if constexpr (!(DIAG & 8)) mfma_acc(acc[j][i], wf[4 * h + j], gf[n & 3]);
-      if (n + 3 < 32) gf[(n + 3) & 3] = gread(u, n + 3);
-      else if (!last1) gf[(n + 3) & 3] = gread(u + 1, n + 3 - 32);
-    }
-    if ((u & 7) == 7) stamp();
-  };
-  for (int u = 0; u < 30; u += 3) {
-    unit(u, W[0], W[2], false, false);
-    unit(u + 1, W[1], W[0], false, false);
-    unit(u + 2, W[2], W[1], false, u + 2 >= 30);
-  }
-  unit(30, W[0], W[2], false, true);
-  unit(31, W[1], W[0], true, true);
-
-  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[m = i*16 + lane%16][n = 64w + j*16 + (lane/16)*4 + e]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)  // MFMA -> VALU read of the accumulators
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
-                 : "+a"(acc[j][0]), "+a"(acc[j][1]), "+a"(acc[j][2]), "+a"(acc[j][3]), "+a"(acc[j][4]),
-                   "+a"(acc[j][5]), "+a"(acc[j][6]), "+a"(acc[j][7]), "+a"(acc[j][8]), "+a"(acc[j][9]),
-                   "+a"(acc[j][10]), "+a"(acc[j][11]), "+a"(acc[j][12]), "+a"(acc[j][13]), "+a"(acc[j][14]),
-                   "+a"(acc[j][15]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live, WV is dead)
-  const int nb = w * 64 + (lane >> 4) * 4;
-  f32x4 bb[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bb[j] = *(const f32x4*)(EP + nb + j * 16);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) t += acc[j][i] + bb[j];
-    float sum = t[0] + t[1] + t[2] + t[3];
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 4 + w] = sum;
-  }
-  __syncthreads();
-  float mean[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 4);
-    mean[i] = (pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / BN);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 d = acc[j][i] + bb[j] - mean[i];
-      t += d * d;
-    }
-    float ss = t[0] + t[1] + t[2] + t[3];
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 4 + w] = ss;
-  }
-  __syncthreads();
-  f32x4 gg[4], ee[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    gg[j] = *(const f32x4*)(EP + 256 + nb + j * 16);
-    ee[j] = *(const f32x4*)(EP + 512 + nb + j * 16);
-  }
-  // 16-B stores: for column blocks (j, j+1) a lane of row group R (= lane/16) holds channels 4R..4R+3
-  // of both; v_permlane16_swap trades block j+1 of even groups for block j of odd groups, so even
-  // groups own 8 consecutive channels of block j, odd groups of block j+1 (32 stores per lane, not 64)
-  bf16* obase = out + (int64_t)s * out_seq_stride;
-  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
-  const int R = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 pr = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 4);
-    const float rstd = rsqrtf((pr[0] + pr[1] + pr[2] + pr[3]) * (1.0f / (BN - 1)) + 1e-5f);
-    const int t = t0 + i * 16 + (lane & 15);
-    uint32_t pk[4][2];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 v = (acc[j][i] + bb[j] - mean[i]) * rstd * gg[j] + ee[j];
-      pk[j][0] = relu_bf16x2(v[0], v[1]);
-      pk[j][1] = relu_bf16x2(v[2], v[3]);
-    }
-#pragma unroll
-    for (int jp = 0; jp < 4; jp += 2) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(pk[jp][d], pk[jp + 1][d], false, false);
-        pk[jp][d] = sw[0];
-        pk[jp + 1][d] = sw[1];
-      }
-      const int col = w * 64 + (jp + (R & 1)) * 16 + (R >> 1) * 8;
-      const u32x4 o = {pk[jp][0], pk[jp][1], pk[jp + 1][0], pk[jp + 1][1]};
-      buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
-    }
-  }
-  if constexpr (STAMPS) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
-    if (samp >= 0 && tid == 0)
-      for (int k = 0; k < 24 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
-  }
-}
-
-
-// ------------------------------------------------------------------------------------------
-// v10 (default): v9's slice pipeline with EIGHT waves, two per SIMD.
-// v9 runs one wave per SIMD, so everything that is not an MFMA -- the slice production (SV reads,
-// conv0 MFMAs, ReLU / packing, LDS stores), the W1 loads, the unit barriers -- sits in the one
-// instruction stream of its SIMD: 3.4k cycles per unit against 2,048 of MFMA.  Here wave w owns
-// output channels 32w .. 32w+31 for all 256 rows (16 x 2 MFMA tiles, 128 accumulators in AGPRs, so
-// two waves fit a SIMD's 512 registers) and the partner wave's MFMAs fill the gaps one wave leaves.
-//   * W1 fragments stay unique per wave (no wave pair shares a column), so the L2 W1 stream is v9's;
-//     each G fragment now feeds two MFMAs instead of four (LDS reads 128 B / cycle / CU at the MFMA
-//     rate, half the array's peak);
-//   * slice work is split by (channel tile ct = w & 1, position tiles w/2 + 4x; waves 0 and 1 also
-//     make tile 16): 4-5 conv0 MFMAs per wave and unit instead of 10;
-//   * ChannelNorm-1 row statistics reduce over 8 partials (one per wave) through LDS.
-// Same per-accumulator k order as v9 (only the ChannelNorm partial sums are grouped differently).
 // ------------------------------------------------------------------------------------------
 constexpr int K_OFF_G = 0;                                    // 3 slots of 272 x 64 B
 constexpr int K_OFF_RED = 3 * I_GSLOT;                        // 52224: [256 rows][8 waves] f32 (epilogue)
@@ -738,317 +90,9 @@ constexpr int K_OFF_SV = K_OFF_RED + BM2 * 8 * 4;             // 60416
 constexpr int K_OFF_C0 = K_OFF_SV + I_SVN * 64;               // 130048
 constexpr int K_OFF_BE = K_OFF_C0 + 256 * 64;                 // 146432
 constexpr int K_LDS = K_OFF_BE + 4 * 256 * 4;                 // 150528
-static_assert(K_OFF_WV + WSEG2 * 4 <= K_OFF_SV, "conv01 v10 waveform alias");
-static_assert(K_LDS <= 163840, "conv01 v10 LDS");
+static_assert(K_OFF_WV + WSEG2 * 4 <= K_OFF_SV, "conv01 waveform alias");
+static_assert(K_LDS <= 163840, "conv01 LDS");
 
-template <bool STAMPS>
-__global__ __launch_bounds__(512, 1) void conv01k_kernel(const float* __restrict__ wav, int64_t N, int L0,
-                                                        const chunk16* __restrict__ c0w, const float* __restrict__ c0stat,
-                                                        const float* __restrict__ beta0, const bf16* __restrict__ W1,
-                                                        const float* __restrict__ b1, const float* __restrict__ g1,
-                                                        const float* __restrict__ be1, bf16* __restrict__ out,
-                                                        int64_t out_seq_stride, int r0, int r1) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[K_LDS];
-  unsigned char* G = smem + K_OFF_G;
-  unsigned char* SV = smem + K_OFF_SV;
-  unsigned char* C0 = smem + K_OFF_C0;
-  float* BE = (float*)(smem + K_OFF_BE);
-  float* EP = BE + 256;
-  float* WV = (float*)(smem + K_OFF_WV);
-  float* red = (float*)(smem + K_OFF_RED);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32w..32w+31, all 256 rows
-  const int ct = w & 1, pq = w >> 1;                        // slice work: channel tile, position tiles pq + 4x
-  const bool p16 = w < 2;                                   // ... and tile 16 (rows 256.., read by row 255 only)
-  const int s = blockIdx.y;
-  const int t0 = r0 + blockIdx.x * BM2;
-  const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
-  unsigned long long stv[8];
-  int nst = 0;
-  auto stamp = [&]() {
-    if constexpr (STAMPS) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (nst < 8) stv[nst] = __builtin_amdgcn_s_memtime();
-      ++nst;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  stamp();
-
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W1, 64 * 256 * 64);
-  const uint32_t wlo = (uint32_t)(((w * 32 + (lane & 15)) * 4 + (lane >> 4)) * 16);
-  auto wload = [&](int u, chunk16* wf) {  // unit u: [h * 2 + j] = k-step (u, h), column tile j
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kk = ((u >> 3) + 4 * h) * 8 + (u & 7);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) wf[h * 2 + j] = buf_load16(wrs, wlo, (uint32_t)(kk * 16384 + j * 1024));
-    }
-  };
-
-  // ---------------- prologue
-  {
-    const __amdgpu_buffer_rsrc_t wr = make_rsrc(wav + (int64_t)s * N, (uint32_t)(N * 4));
-    const int xb = 20 * t0 - 13;  // first sample of the segment (negative offsets read as zero)
-    uint32_t wv[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k)
-      wv[k] = __builtin_amdgcn_raw_buffer_load_b32(wr, (int)((uint32_t)(xb + tid + 512 * k) * 4u), 0, 0);
-    chunk16 c0[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) c0[i] = c0w[tid + i * 512];
-    f32x4 ep = {0.f, 0.f, 0.f, 0.f};
-    if (tid < 64) ep = ((const f32x4*)beta0)[tid];
-    else if (tid < 128) ep = ((const f32x4*)b1)[tid - 64];
-    else if (tid < 192) ep = ((const f32x4*)g1)[tid - 128];
-    else if (tid < 256) ep = ((const f32x4*)be1)[tid - 192];
-#pragma unroll
-    for (int k = 0; k < 11; ++k)
-      if (tid + 512 * k < WSEG2) WV[tid + 512 * k] = __builtin_bit_cast(float, wv[k]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) ((chunk16*)C0)[tid + i * 512] = c0[i];
-    if (tid < 256) ((f32x4*)BE)[tid] = ep;
-  }
-  chunk16 W[3][4];  // W1 register ring: unit u in set u % 3
-  wload(0, W[0]);
-  wload(1, W[1]);
-  __syncthreads();
-
-  for (int j = tid; j < I_SVN; j += 512) {
-    const int r = j / NPOS2, i = j - r * NPOS2;
-    const int p = 4 * (t0 + i) - 2 + r;
-    const bool valid = i < GROWS2 && p >= 0 && p < L0;
-    float sm[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) sm[k] = WV[min(20 * i + 5 * r + k, WSEG2 - 1)];
-    float q = c0stat[C0Stat::BETA];
-#pragma unroll
-    for (int a = 0; a < 10; ++a) {
-      float ga = fmaf(c0stat[C0Stat::G + a * 10 + a], sm[a], 2.0f * c0stat[C0Stat::H + a]);
-#pragma unroll
-      for (int b = a + 1; b < 10; ++b) ga = fmaf(2.0f * c0stat[C0Stat::G + a * 10 + b], sm[b], ga);
-      q = fmaf(ga, sm[a], q);
-    }
-    const float rs = valid ? rsqrtf(fmaxf(q, 0.f) * (1.0f / 255.0f) + 1e-5f) : 0.f;
-    bf16 hi[10], lo[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const float x = rs * sm[k];
-      hi[k] = (bf16)x;
-      lo[k] = (bf16)(x - (float)hi[k]);
-    }
-    const bf16 rb = (bf16)rs;
-    const bf16x8 v[4] = {{hi[0], hi[1], hi[2], hi[3], hi[4], hi[5], hi[6], hi[7]},
-                         {hi[8], hi[9], lo[0], lo[1], lo[2], lo[3], lo[4], lo[5]},
-                         {lo[6], lo[7], lo[8], lo[9], hi[0], hi[1], hi[2], hi[3]},
-                         {hi[4], hi[5], hi[6], hi[7], hi[8], hi[9], rb, rb}};
-    unsigned char* row = SV + j * 64;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) *(bf16x8*)(row + sphys(j, c) * 16) = v[c];
-  }
-
-  // validity of this lane's position in slice tile x (pq + 4x, x < 4; 16 for x = 4) of phase r: bit 5r + x
-  uint32_t vmask = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int x = 0; x < 5; ++x) {
-      const int pt = x == 4 ? 16 : pq + 4 * x;
-      const int p = 4 * (t0 + pt * 16 + (lane & 15)) - 2 + r;
-      vmask |= (uint32_t)(p >= 0 && p < L0) << (5 * r + x);
-    }
-  __syncthreads();
-
-  // ---- slice v (phase v>>3, channel group v&7) -> slot v%3; this wave makes channel tile ct
-  auto read_c0 = [&](int v, chunk16& c0, f32x4& bt) {
-    const int g = v & 7;
-    c0 = ((const chunk16*)C0)[((2 * g + ct) * 16 + (lane & 15)) * 4 + (lane >> 4)];
-    bt = *(const f32x4*)(BE + (2 * g + ct) * 16 + 4 * (lane >> 4));
-  };
-  auto read_sv = [&](int v, int x) -> chunk16 {
-    const int pt = x == 4 ? 16 : pq + 4 * x;
-    const int jj = ((v >> 3) & 3) * NPOS2 + pt * 16 + (lane & 15);
-    return *(const chunk16*)(SV + jj * 64 + sphys(jj, lane >> 4) * 16);
-  };
-  auto pstore = [&](int v, int x, const f32x4& z) {
-    const int pt = x == 4 ? 16 : pq + 4 * x;
-    const int prow = pt * 16 + (lane & 15);
-    const uint32_t m = 0u - ((vmask >> (5 * ((v >> 3) & 3) + x)) & 1u);
-    unsigned char* gs = G + (v % 3) * I_GSLOT;
-    const u32x2 o = {relu_bf16x2(z[0], z[1]) & m, relu_bf16x2(z[2], z[3]) & m};
-    const int lc = 2 * ct + (lane >> 5);
-    *(u32x2*)(gs + prow * 64 + sphys(prow, lc) * 16 + ((lane >> 4) & 1) * 8) = o;
-  };
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {  // slices 0 and 1
-    chunk16 c0;
-    f32x4 bt;
-    read_c0(v, c0, bt);
-#pragma unroll
-    for (int x = 0; x < 5; ++x) {
-      if (x == 4 && !p16) break;
-      const chunk16 sv = read_sv(v, x);
-      pstore(v, x, mfma_chunk<bf16>(c0, sv, bt));
-    }
-  }
-
-  f32x4 acc[2][16];  // [n tile][m tile] of C^T, in AGPRs
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto gread = [&](int u, int n) -> chunk16 {  // n = 16h + i -> k-step (u,h), row block i
-    const unsigned char* gs = G + (u % 3) * I_GSLOT;
-    const int row = (n & 15) * 16 + (lane & 15) + (n >> 4);
-    return *(const chunk16*)(gs + row * 64 + sphys(row, lane >> 4) * 16);
-  };
-  chunk16 gf[4];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // slices 0, 1 published; WV (slot 2) free
-#pragma unroll
-  for (int n = 0; n < 3; ++n) gf[n] = gread(0, n);
-  stamp();
-
-  auto unit = [&](const int u, chunk16* wf, chunk16* wn2, const bool last1, const bool last2) {
-    // B_u: own slice u+1 stores retired; W1 of unit u landed (unit u+1's 4 loads are younger)
-    __builtin_amdgcn_sched_barrier(0);
-    if (last1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (!last2) wload(u + 2, wn2);
-    const int v = u + 2;
-    chunk16 c0, sv;
-    f32x4 bt, z;
-    read_c0(v, c0, bt);
-#pragma unroll
-    for (int n = 0; n < 32; ++n) {
-      __builtin_amdgcn_sched_barrier(0);
-      // slice v: tile x operands at group 7x, MFMA at 7x+2, store at 7x+4 (tile 16: 28 / 30 / 31)
-      if (n % 7 == 0 && n / 7 < 4) sv = read_sv(v, n / 7);
-      if (n % 7 == 2 && n / 7 < 4) z = mfma_chunk<bf16>(c0, sv, bt);
-      if (n % 7 == 4 && n / 7 < 4) pstore(v, n / 7, z);
-      if (p16) {
-        if (n == 28) sv = read_sv(v, 4);
-        if (n == 30) z = mfma_chunk<bf16>(c0, sv, bt);
-        if (n == 31) pstore(v, 4, z);
-      }
-      const int i = n & 15, h = n >> 4;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) mfma_acc(acc[j][i], wf[2 * h + j], gf[n & 3]);
-      if (n + 3 < 32) gf[(n + 3) & 3] = gread(u, n + 3);
-      else if (!last1) gf[(n + 3) & 3] = gread(u + 1, n + 3 - 32);
-    }
-    if ((u & 7) == 7) stamp();
-  };
-  for (int u = 0; u < 30; u += 3) {
-    unit(u, W[0], W[2], false, false);
-    unit(u + 1, W[1], W[0], false, false);
-    unit(u + 2, W[2], W[1], false, u + 2 >= 30);
-  }
-  unit(30, W[0], W[2], false, true);
-  unit(31, W[1], W[0], true, true);
-
-  // ---------------- epilogue: + b1, ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
-  // lane holds C[m = i*16 + lane%16][n = 32w + j*16 + (lane/16)*4 + e]
-#pragma unroll
-  for (int j = 0; j < 2; ++j)  // MFMA -> VALU read of the accumulators
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
-                 : "+a"(acc[j][0]), "+a"(acc[j][1]), "+a"(acc[j][2]), "+a"(acc[j][3]), "+a"(acc[j][4]),
-                   "+a"(acc[j][5]), "+a"(acc[j][6]), "+a"(acc[j][7]), "+a"(acc[j][8]), "+a"(acc[j][9]),
-                   "+a"(acc[j][10]), "+a"(acc[j][11]), "+a"(acc[j][12]), "+a"(acc[j][13]), "+a"(acc[j][14]),
-                   "+a"(acc[j][15]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave done with the slots (red overlaps nothing live)
-  const int nb = w * 32 + (lane >> 4) * 4;
-  f32x4 bb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) bb[j] = *(const f32x4*)(EP + nb + j * 16);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 t = acc[0][i] + bb[0] + acc[1][i] + bb[1];
-    float sum = t[0] + t[1] + t[2] + t[3];
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 8 + w] = sum;
-  }
-  __syncthreads();
-  float mean[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 pa = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8);
-    const f32x4 pb = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8 + 4);
-    mean[i] = ((pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]))) * (1.0f / BN);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 d0 = acc[0][i] + bb[0] - mean[i], d1 = acc[1][i] + bb[1] - mean[i];
-    const f32x4 t = d0 * d0 + d1 * d1;
-    float ss = t[0] + t[1] + t[2] + t[3];
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if ((lane >> 4) == 0) red[(i * 16 + (lane & 15)) * 8 + w] = ss;
-  }
-  __syncthreads();
-  f32x4 gg[2], ee[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    gg[j] = *(const f32x4*)(EP + 256 + nb + j * 16);
-    ee[j] = *(const f32x4*)(EP + 512 + nb + j * 16);
-  }
-  // 16-B stores: v_permlane16_swap trades column block 1 of even row groups for block 0 of odd ones,
-  // so even groups own 8 consecutive channels of block 0, odd groups of block 1
-  bf16* obase = out + (int64_t)s * out_seq_stride;
-  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)r1 * BN * 2));
-  const int R = lane >> 4;
-  const int col = w * 32 + (R & 1) * 16 + (R >> 1) * 8;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f32x4 pa = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8);
-    const f32x4 pb = *(const f32x4*)(red + (i * 16 + (lane & 15)) * 8 + 4);
-    const float var = (pa[0] + pa[1]) + (pa[2] + pa[3]) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
-    const float rstd = rsqrtf(var * (1.0f / (BN - 1)) + 1e-5f);
-    const int t = t0 + i * 16 + (lane & 15);
-    uint32_t pk[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const f32x4 v = (acc[j][i] + bb[j] - mean[i]) * rstd * gg[j] + ee[j];
-      pk[j][0] = relu_bf16x2(v[0], v[1]);
-      pk[j][1] = relu_bf16x2(v[2], v[3]);
-    }
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][d], pk[1][d], false, false);
-      pk[0][d] = sw[0];
-      pk[1][d] = sw[1];
-    }
-    const u32x4 o = {pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
-    buf_store16(orsc, t < r1 ? (uint32_t)(((int64_t)t * BN + col) * 2) : 0xFFFFFFF0u, o);
-  }
-  if constexpr (STAMPS) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp();
-    if (samp >= 0 && tid == 0)
-      for (int k = 0; k < 8 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// v11 (default): v10 with the conv1 k-steps on v_mfma_f32_32x32x16_bf16.
-// v10's units ran at ~71 % of MFMA issue, issue-bound: a 16x16x32 MFMA leaves 8 of its 16 cycles to
-// the SIMD's other instructions, and a unit carries ~100 of them per wave (G reads, waits, slice
-// work).  A 32x32x16 leaves 24 of 32 for the same k-work (half the MFMA instructions, the same G /
-// W1 fragment count: a 32-row x 16-k fragment is 1 KiB like a 16 x 32 one).
-//   * wave w: 8 row tiles of 32 x one 32-channel column tile (8 x 16 accumulators in AGPRs);
-//   * G slots use the swizzle chunk' = (chunk + row/4) mod 4: conflict-free ds_read_b128 for 32
-//     consecutive rows (either tap offset) and for the slice stores of 16 rows (v10's swizzle was
-//     2-way conflicted on the stores);
-//   * epilogue rows are one lane each (row = lane % 32 of a row tile, 16 channels per lane, the
-//     other 16 in lane ^ 32): row sums by one shuffle, 16-B stores via v_permlane32_swap.
-// ------------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VAP_DEV int gphys(int row, int c) { return (c + (row >> 2)) & 3; }
 VAP_DEV int c1_lane() {  // the lane id by volatile asm: values derived from it are not hoisted
@@ -1386,58 +430,12 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
   if (r1 < 0) r1 = L1;
   if (S <= 0 || L1 <= 0 || r0 < 0 || r1 > L1 || r0 >= r1) return hipErrorInvalidValue;
   static const bool stamps = getenv("VAP_CONV01_STAMPS") != nullptr;
-  static const bool v2 = getenv("VAP_CONV01_V2") != nullptr;  // the whole-phase-image kernel (previous default)
-  if (v2) {
-    dim3 grid((r1 - r0 + BM - 1) / BM, S);
-    if (stamps)
-      hipLaunchKernelGGL(conv01b_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
-                         b1, g1, be1, out, out_seq_stride, r0, r1);
-    else
-      hipLaunchKernelGGL(conv01b_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
-                         W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
-    return hipGetLastError();
-  }
-  dim3 grid((r1 - r0 + BM2 - 1) / BM2, S);
-  static const bool v9 = getenv("VAP_CONV01_V9") != nullptr;    // the four-wave kernel
-  static const bool v10 = getenv("VAP_CONV01_V10") != nullptr;  // eight waves, 16x16x32 conv1 MFMAs
-  if (!v9 && !v10) {
-    if (stamps)
-      hipLaunchKernelGGL(conv01m_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
-                         b1, g1, be1, out, out_seq_stride, r0, r1);
-    else
-      hipLaunchKernelGGL(conv01m_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
-                         W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
-    return hipGetLastError();
-  }
-  if (!v9) {
-    if (stamps)
-      hipLaunchKernelGGL(conv01k_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
-                         b1, g1, be1, out, out_seq_stride, r0, r1);
-    else
-      hipLaunchKernelGGL(conv01k_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s, b1,
-                       g1, be1, out, out_seq_stride, r0, r1);
-    return hipGetLastError();
-  }
-  static const int diag = getenv("VAP_CONV01_DIAG") ? atoi(getenv("VAP_CONV01_DIAG")) : 0;
-  if (stamps && diag) {  // timing diagnostics only: the outputs are garbage
-#define VAP_DIAG_CASE(D)                                                                                          \
-  case D:                                                                                                         \
-    hipLaunchKernelGGL((conv01i_kernel<true, D>), grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, \
-                       beta0, W1s, b1, g1, be1, out, out_seq_stride, r0, r1);                                     \
-    break;
-    switch (diag) {
-      VAP_DIAG_CASE(2) VAP_DIAG_CASE(4) VAP_DIAG_CASE(6) VAP_DIAG_CASE(8) VAP_DIAG_CASE(20) VAP_DIAG_CASE(36)
-      VAP_DIAG_CASE(68)
-      default: break;
-    }
-#undef VAP_DIAG_CASE
-    return hipGetLastError();
-  }
+  const dim3 grid((r1 - r0 + BM2 - 1) / BM2, S);
   if (stamps)
-    hipLaunchKernelGGL(conv01i_kernel<true>, grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
-                       W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
+    hipLaunchKernelGGL(conv01m_kernel<true>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0, W1s,
+                       b1, g1, be1, out, out_seq_stride, r0, r1);
   else
-    hipLaunchKernelGGL(conv01i_kernel<false>, grid, dim3(256), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
+    hipLaunchKernelGGL(conv01m_kernel<false>, grid, dim3(512), 0, st, wav, N, L0, (const chunk16*)c0w, c0stat, beta0,
                        W1s, b1, g1, be1, out, out_seq_stride, r0, r1);
   return hipGetLastError();
 }

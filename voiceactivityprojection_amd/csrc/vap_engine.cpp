@@ -53,7 +53,6 @@ struct vap_handle {
   // micro-batch pipeline: side streams for the LSTM recurrences + events
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
-  bool legacy_tr = false;  // VAP_LEGACY_TR=1: bf16 transformer on LN kernel + general GEMM (A/B testing)
   double tc_edge = 0.0;             // time chunks: first / last chunk fraction of the frames (0: even split)
   // forward: front-end / back-end boundaries (cumulative frame fractions, VAP_TC_FE / VAP_TC_BE;
   // "" = the even time_chunks split for both)
@@ -66,12 +65,6 @@ struct vap_handle {
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
-  bool lnproj_fused = true;  // bf16: LN + QKV (+ raw cross K/V) and out-proj + LN + cross Q as single
-                             // launches (k_block.hip lnproj); VAP_LNPROJ=0 selects the row-panel kernels
-  bool block_fused = true;  // bf16: last out-projection + residual + LN + FFN + residual in one launch
-                            // (k_block.hip); VAP_BLOCK=0 selects the separate row-panel + FFN kernels
-  bool ffn_fused = true;  // bf16 FFN with the hidden in LDS (k_ffn.hip): 62 us vs 93 us for the unfused
-                          // row-panel up + GEMM down per 32k rows; VAP_FFN_FUSED=0 selects the unfused pair
   hipStream_t side[NSIDE] = {};
   // time-pipelined forward: conv2..4 + gate projections of each front-end piece on this high-priority
   // stream while the caller stream runs the next piece's conv01, so each launch's last partial round
@@ -80,7 +73,6 @@ struct vap_handle {
   // forwards without per-launch timing events; one stream keeps each kernel's events clean)
   hipStream_t fe_stream = nullptr;
   int fe_streams = 1;
-  bool heads_fused = true;  // VAP_HEADS_FUSED=0: combinator + vap_head as three GEMM launches
   bool fe_first_serial = false;
   int fe_gate = 0;  // VAP_FE_GATE: see conv_rows
   bool fe_align = true;  // VAP_FE_ALIGN=0: conv1..3 ranges per piece exactly what its conv4 rows need
@@ -319,15 +311,19 @@ Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross
   p.H0 = take(S * p.sh * es);
   p.H1 = take(S * p.sh * es);
   p.X = take(S * T * D * sizeof(float));
-  p.LN = take(S * T * D * es);
+  // bf16 mode: LayerNorm, FFN hidden and combinator rows stay on chip (fused row kernels of
+  // k_block.hip), so LN / FF / HC / HCT are fp32-mode buffers; the time-chunked schedule keeps Q/K/V
+  // per layer (QKVL / KVCL) instead of QKV / KVC
+  const bool fp = es == 4, tc = kv_self_layers > 0;
+  p.LN = take(fp ? S * T * D * es : 0);
   p.RAW = take(S * T * D * es);
-  p.QKV = take(S * T * 3 * D * es);
-  p.KVC = take(S * T * 2 * D * es);
+  p.QKV = take(tc ? 0 : S * T * 3 * D * es);
+  p.KVC = take(tc ? 0 : S * T * 2 * D * es);
   p.QC = take(S * T * D * es);
   p.ATT = take(S * T * D * es);
-  p.FF = take(S * T * 3 * D * es);
-  p.HC = take((size_t)B * T * D * sizeof(float));
-  p.HCT = take((size_t)B * T * D * es);
+  p.FF = take(fp ? S * T * 3 * D * es : 0);
+  p.HC = take(fp ? (size_t)B * T * D * sizeof(float) : 0);
+  p.HCT = take(fp ? (size_t)B * T * D * es : 0);
   if (kv_self_layers) p.QKVL = take((size_t)kv_self_layers * S * T * 3 * D * es);
   if (kv_cross_layers) p.KVCL = take((size_t)kv_cross_layers * S * T * 2 * D * es);
   p.total = o;
@@ -596,8 +592,13 @@ int attn_maps(vap_handle* h, const AttnArgs& a, int which, int layer, Range r, h
   return VAP_OK;
 }
 
-int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
-                hipStream_t st, int layer) {
+// bf16 transformer layer (modules.py:246-275) on the fused row kernels of k_block.hip, over the
+// contiguous rows of a clip range:
+//   lnproj: LN_self + Q/K/V (+ the raw-row cross K/V: modules.py:265-272 take the UN-normalised x)
+//   attn3:  self attention;  [stereo] lnproj: out-proj + residual + LN_src + cross Q;  attn3: cross
+//   block:  last out-projection + residual + LN + FFN + residual
+int tr_layer_bf16(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
+                  hipStream_t st, int layer) {
   using T = bf16;
   const int T_ = p.T;
   const int S = r.ns();
@@ -608,22 +609,21 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   T* KVC = (T*)(ws + p.KVC) + so * 2 * D;
   T* QC = (T*)(ws + p.QC) + so * D;
   T* ATT = (T*)(ws + p.ATT) + so * D;
-  T* FF = (T*)(ws + p.FF) + so * 3 * D;
   const int H = h->dims.num_heads;
   const float scale = 1.0f / std::sqrt((float)D);
   const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
-  auto rp = [&](const void* A, int64_t lda, const std::string& w, int N, void* C, int64_t ldc, const float* add,
-                const std::string& ln, int amode, int epi) {
-    RowPanelArgs a{A, lda, rows, h->W<T>(w + "@rp"), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
-                   ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
-    a.w_packed = 1;
-    return launch_rowpanel(a, amode, epi, st);
+  auto lnp = [&](const T* o, const std::string& wo, const std::string& wp, int np, T* cp, int64_t ldp,
+                 const std::string& wr, int nr, T* cr, int64_t ldr, const std::string& ln) {
+    LnProjArgs a{};
+    a.x = X; a.o = o; a.M = rows; a.rows_per_seq = 0; a.x_seq = t1; a.o_seq = t1;
+    a.Wo = o ? h->W<T>(wo + "@rp") : nullptr; a.Wp = h->W<T>(wp + "@rp"); a.Wr = nr ? h->W<T>(wr + "@rp") : nullptr;
+    a.cp = cp; a.ldp = ldp; a.cp_seq = (int64_t)T_ * ldp; a.cr = cr; a.ldr = ldr; a.cr_seq = (int64_t)T_ * ldr;
+    a.gamma = h->P(ln + ".weight"); a.beta = h->P(ln + ".bias"); a.eps = 1e-5f; a.np = np; a.nr = nr;
+    return launch_lnproj(a, st);
   };
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(X, D, pre + ".qkv", 3 * D, QKV, 3 * D, nullptr, pre + ".ln_self_attn", 1, 0));
-    if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
-      HIPCHK(rp(X, D, pre + ".kvc", 2 * D, KVC, 2 * D, nullptr, "", 2, 0));
+    HIPCHK(lnp(nullptr, "", pre + ".qkv", 3, QKV, 3 * D, pre + ".kvc", cross ? 2 : 0, KVC, 2 * D, pre + ".ln_self_attn"));
   }
   {
     Timed tm(h, VAP_K_ATTN, st);
@@ -632,16 +632,10 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     HIPCHK(launch_attention<T>(a, st));
     if (int rc = attn_maps<T>(h, a, cross ? 2 : 0, layer, r, st)) return rc;
   }
-  // the layer's last out-projection goes into the fused block kernel with the FFN
-  const bool blk = h->block_fused && h->ffn_fused;
-  if (cross || !blk) {
-    Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(ATT, D, pre + ".o", D, X, D, X, "", 0, 2));
-  }
   if (cross) {
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(rp(X, D, pre + ".qc", D, QC, D, nullptr, pre + ".ln_src_attn", 1, 0));
+      HIPCHK(lnp(ATT, pre + ".o", pre + ".qc", 1, QC, D, "", 0, nullptr, 0, pre + ".ln_src_attn"));
     }
     {
       Timed tm(h, VAP_K_ATTN, st);
@@ -650,29 +644,12 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       HIPCHK(launch_attention<T>(a, st));
       if (int rc = attn_maps<T>(h, a, 1, layer, r, st)) return rc;
     }
-    if (!blk) {
-      Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(rp(ATT, D, pre + ".oc", D, X, D, X, "", 0, 2));
-    }
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    if (blk) {
-      BlockArgs b{X, ATT, rows, 0, 0, 0, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")), h->W<T>(pre + ".w1@rp"),
-                  h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"), h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
-      HIPCHK(launch_block(b, 0, st));
-    } else if (h->ffn_fused) {
-      FfnArgs f{X, rows, 0, 0, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
-                h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
-      HIPCHK(launch_ffn(f, st));
-    } else {
-      HIPCHK(rp(X, D, pre + ".w1", 3 * D, FF, 3 * D, nullptr, pre + ".ln_ffnetwork", 1, 1));
-      GemmArgs g2 = gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1);
-      g2.add = X;
-      g2.ld_add = D;
-      g2.add_seq_stride = t1;
-      HIPCHK(gemm<T>(g2, st, true));
-    }
+    BlockArgs b{X, ATT, rows, 0, 0, 0, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")), h->W<T>(pre + ".w1@rp"),
+                h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"), h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
+    HIPCHK(launch_block(b, 0, st));
   }
   return VAP_OK;
 }
@@ -680,9 +657,7 @@ int tr_layer_rp(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
 template <typename T>
 int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, Range r,
              hipStream_t st, int layer) {
-  if constexpr (sizeof(T) == 2) {
-    if (!h->legacy_tr) return tr_layer_rp(h, p, ws, pre, cross, r, st, layer);
-  }
+  if constexpr (sizeof(T) == 2) return tr_layer_bf16(h, p, ws, pre, cross, r, st, layer);
   const int T_ = p.T;
   const int S = r.ns();
   const int64_t rows = (int64_t)S * T_;
@@ -883,7 +858,7 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
   float* HC = (float*)(ws + p.HC) + r.c0 * t1;
   T* HCT = (T*)(ws + p.HCT) + r.c0 * t1;
   if constexpr (sizeof(T) == 2) {
-    if (h->heads_fused) {  // combinator + vap_head in one launch (k_block.hip heads_kernel)
+    {  // combinator + vap_head + va_classifier in one launch (k_block.hip heads_kernel)
       Timed tm(h, VAP_K_HEADS, st);
       if (!raw_ready) HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));
       HeadsArgs ha{(const bf16*)RAW, t1, r.nc * T_, T_, (const bf16*)h->W<T>("comb_a@rp"), (const bf16*)h->W<T>("comb_b@rp"),
@@ -981,20 +956,8 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
   T* KVC = (T*)(ws + p.KVCL) + (int64_t)ci * S * t2;
   T* QC = (T*)(ws + p.QC);
   T* ATT = (T*)(ws + p.ATT);
-  T* FF = (T*)(ws + p.FF);
   const int H = h->dims.num_heads;
   const float scale = 1.0f / std::sqrt((float)D);
-  // row-panel over rows (s, t in [f0, f1)); A / C point at row f0 of sequence 0
-  auto rp = [&](const void* A, int64_t lda, int64_t aseq, const std::string& w, int N, void* C, int64_t ldc,
-                int64_t cseq, const float* add, const std::string& ln, int amode, int epi) {
-    RowPanelArgs a{A, lda, S * nf, h->W<T>(w + "@rp"), D, N, C, ldc, add, ln.empty() ? nullptr : h->P(ln + ".weight"),
-                   ln.empty() ? nullptr : h->P(ln + ".bias"), 1e-5f};
-    a.w_packed = 1;
-    a.rows_per_seq = nf;
-    a.a_seq = aseq;
-    a.c_seq = cseq;
-    return launch_rowpanel(a, amode, epi, st);
-  };
   float* Xf = X + (int64_t)f0 * D;
   // fused LN projections (k_block.hip): rows (s, t in [f0, f1)), x / o / outputs at row f0 of sequence 0
   auto lnp = [&](const T* o, const std::string& wo, const std::string& wp, int np, T* cp, int64_t ldp, int64_t cpseq,
@@ -1006,17 +969,10 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     a.gamma = h->P(ln + ".weight"); a.beta = h->P(ln + ".bias"); a.eps = 1e-5f; a.np = np; a.nr = nr;
     return launch_lnproj(a, st);
   };
-  const bool lnpf = h->lnproj_fused;
   {
-    Timed tm(h, VAP_K_TR_GEMM, st);
-    if (lnpf) {  // LN + QKV and the raw-row cross K/V from one read of x
-      HIPCHK(lnp(nullptr, "", pre + ".qkv", 3, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, pre + ".kvc", cross ? 2 : 0,
-                 KVC + (int64_t)f0 * 2 * D, 2 * D, t2, pre + ".ln_self_attn"));
-    } else {
-      HIPCHK(rp(Xf, D, t1, pre + ".qkv", 3 * D, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_self_attn", 1, 0));
-      if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
-        HIPCHK(rp(Xf, D, t1, pre + ".kvc", 2 * D, KVC + (int64_t)f0 * 2 * D, 2 * D, t2, nullptr, "", 2, 0));
-    }
+    Timed tm(h, VAP_K_TR_GEMM, st);  // LN + QKV and the raw-row cross K/V from one read of x
+    HIPCHK(lnp(nullptr, "", pre + ".qkv", 3, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, pre + ".kvc", cross ? 2 : 0,
+               KVC + (int64_t)f0 * 2 * D, 2 * D, t2, pre + ".ln_self_attn"));
   }
   {
     Timed tm(h, VAP_K_ATTN, st);
@@ -1025,19 +981,11 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     a.q0 = f0;
     HIPCHK(launch_attention<T>(a, st));
   }
-  const bool blk = h->block_fused && h->ffn_fused;  // last out-projection fused with the FFN
-  if (cross && lnpf) {  // out-proj + residual + LN_src + cross Q
-    Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(lnp(ATT + (int64_t)f0 * D, pre + ".o", pre + ".qc", 1, QC + (int64_t)f0 * D, D, t1, "", 0, nullptr, 0, 0,
-               pre + ".ln_src_attn"));
-  } else if (cross || !blk) {
-    Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".o", D, Xf, D, t1, Xf, "", 0, 2));
-  }
   if (cross) {
-    if (!lnpf) {
-      Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(rp(Xf, D, t1, pre + ".qc", D, QC + (int64_t)f0 * D, D, t1, nullptr, pre + ".ln_src_attn", 1, 0));
+    {
+      Timed tm(h, VAP_K_TR_GEMM, st);  // out-proj + residual + LN_src + cross Q
+      HIPCHK(lnp(ATT + (int64_t)f0 * D, pre + ".o", pre + ".qc", 1, QC + (int64_t)f0 * D, D, t1, "", 0, nullptr, 0, 0,
+                 pre + ".ln_src_attn"));
     }
     {
       Timed tm(h, VAP_K_ATTN, st);
@@ -1046,31 +994,14 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
       a.q0 = f0;
       HIPCHK(launch_attention<T>(a, st));
     }
-    if (!blk) {
-      Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(rp(ATT + (int64_t)f0 * D, D, t1, pre + ".oc", D, Xf, D, t1, Xf, "", 0, 2));
-    }
   }
   {
-    Timed tm(h, VAP_K_TR_GEMM, st);
-    if (blk) {  // out-proj + residual + LN + FFN + residual (k_block.hip)
-      BlockArgs b{Xf, ATT + (int64_t)f0 * D, S * nf, nf, t1, t1, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")),
-                  h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
-                  h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
-      b.xb = xb_out ? xb_out + (int64_t)f0 * D : nullptr;
-      HIPCHK(launch_block(b, 0, st));
-    } else if (h->ffn_fused) {  // LN -> up -> GELU -> down -> +x with the hidden in LDS (k_ffn.hip)
-      FfnArgs f{Xf, S * nf, nf, t1, h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
+    Timed tm(h, VAP_K_TR_GEMM, st);  // out-proj + residual + LN + FFN + residual (k_block.hip)
+    BlockArgs b{Xf, ATT + (int64_t)f0 * D, S * nf, nf, t1, t1, h->W<T>(pre + (cross ? ".oc@rp" : ".o@rp")),
+                h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
-      HIPCHK(launch_ffn(f, st));
-    } else {
-      HIPCHK(rp(Xf, D, t1, pre + ".w1", 3 * D, FF + (int64_t)f0 * 3 * D, 3 * D, t3, nullptr, pre + ".ln_ffnetwork", 1, 1));
-      GemmArgs g2 = gargs(FF + (int64_t)f0 * 3 * D, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, nf, S, Xf, D, t1);
-      g2.add = Xf;
-      g2.ld_add = D;
-      g2.add_seq_stride = t1;
-      HIPCHK(gemm<T>(g2, st, true));
-    }
+    b.xb = xb_out ? xb_out + (int64_t)f0 * D : nullptr;
+    HIPCHK(launch_block(b, 0, st));
   }
   return VAP_OK;
 }
@@ -1277,37 +1208,15 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
   const int64_t t1 = (int64_t)T_ * D;
   float* X = (float*)(ws + p.X);
   T* RAW = (T*)(ws + p.RAW);
-  float* HC = (float*)(ws + p.HC);
-  T* HCT = (T*)(ws + p.HCT);
   Timed tm(h, VAP_K_HEADS, st);
   const int64_t o = (int64_t)f0 * D;
-  if (h->heads_fused) {  // heads_kernel on the frame range [f0, f0 + nf) of every clip
-    HeadsArgs ha{(const bf16*)(RAW + o), t1, B * nf, nf, (const bf16*)h->W<T>("comb_a@rp"),
-                 (const bf16*)h->W<T>("comb_b@rp"), (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"),
-                 h->P("ar.combinator.ln.bias"), h->P("vap_head.bias"), logits, 1e-5f, h->P("va_classifier.weight"),
-                 h->P("va_classifier.bias"), vadl, T_, f0};
-    ha.xf = X + o;
-    HIPCHK(launch_heads(ha, st));
-    return VAP_OK;
-  }
-  GemmArgs ga = gargs(RAW + o, D, 2 * t1, h->W<T>("comb_a"), D, D, nullptr, nf, B, HC + o, D, t1);
-  ga.norm = 2;
-  ga.act = 2;
-  ga.gamma = h->P("ar.combinator.ln.weight");
-  ga.beta = h->P("ar.combinator.ln.bias");
-  HIPCHK(gemm<T>(ga, st, true));
-  GemmArgs gb = ga;
-  gb.A = RAW + t1 + o;
-  gb.W = h->W<T>("comb_b");
-  gb.add = HC + o;
-  gb.ld_add = D;
-  gb.add_seq_stride = t1;
-  HIPCHK(gemm<T>(gb, st, true));
-  HIPCHK(launch_convert_rows<T>(HC + o, t1, HCT + o, t1, B, nf, st));
-  HIPCHK(gemm<T>(gargs(HCT + o, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), nf, B,
-                       logits + (int64_t)f0 * 256, 256, (int64_t)T_ * 256), st, true));
-  HIPCHK(launch_vad_head_rows(X + o, t1, B, T_, f0, nf, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
-                              vadl, st));
+  // heads_kernel on the frame range [f0, f0 + nf) of every clip
+  HeadsArgs ha{(const bf16*)(RAW + o), t1, B * nf, nf, (const bf16*)h->W<T>("comb_a@rp"),
+               (const bf16*)h->W<T>("comb_b@rp"), (const bf16*)h->W<T>("head@rp"), h->P("ar.combinator.ln.weight"),
+               h->P("ar.combinator.ln.bias"), h->P("vap_head.bias"), logits, 1e-5f, h->P("va_classifier.weight"),
+               h->P("va_classifier.bias"), vadl, T_, f0};
+  ha.xf = X + o;
+  HIPCHK(launch_heads(ha, st));
   return VAP_OK;
 }
 
@@ -1347,21 +1256,19 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       HIPCHK(gemm<T>(ga, bst, true));
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
-    const bool hchunk = h->heads_chunked && h->block_fused && h->ffn_fused && h->dims.cross_layers > 0;
+    const bool hchunk = h->heads_chunked && h->dims.cross_layers > 0;
     int li = 0;
     for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
       if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, bst))) return rc;
     for (int l = 0; l < h->dims.cross_layers; ++l, ++li) {
       // the last layer's block kernel also writes x as bf16 (RAW): the combinator's input, so the
       // heads need no separate fp32 -> bf16 pass over x
-      const bool xb_ok = h->block_fused && h->ffn_fused;
-      bf16* xb = xb_ok && l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
+      bf16* xb = l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
       if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst, xb))) return rc;
     }
     if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bst))) return rc;
   }
-  if (!(h->heads_chunked && h->block_fused && h->ffn_fused && h->dims.cross_layers > 0) &&
-      (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst, h->block_fused && h->ffn_fused)))
+  if (!(h->heads_chunked && h->dims.cross_layers > 0) && (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst, true)))
     return rc;
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
@@ -1928,10 +1835,6 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   vap_handle* h = new vap_handle();
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
-  if (const char* e = getenv("VAP_LEGACY_TR")) h->legacy_tr = atoi(e) != 0;
-  if (const char* e = getenv("VAP_FFN_FUSED")) h->ffn_fused = atoi(e) != 0;
-  if (const char* e = getenv("VAP_BLOCK")) h->block_fused = atoi(e) != 0;
-  if (const char* e = getenv("VAP_LNPROJ")) h->lnproj_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_HEADS_CHUNKED")) h->heads_chunked = atoi(e) != 0;
   if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
@@ -1940,7 +1843,6 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_FE_ALIGN")) h->fe_align = atoi(e) != 0;
   if (const char* e = getenv("VAP_FE_FIRST_SERIAL")) h->fe_first_serial = atoi(e) != 0;
   if (const char* e = getenv("VAP_FE_GATE")) h->fe_gate = atoi(e);
-  if (const char* e = getenv("VAP_HEADS_FUSED")) h->heads_fused = atoi(e) != 0;
   if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);

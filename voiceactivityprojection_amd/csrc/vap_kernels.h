@@ -230,52 +230,14 @@ hipError_t launch_conv01(const float* wav, int S, int64_t N, int L0, int L1, con
 // W [N][K] bf16 -> k-step-major [K/32][N][32] (conv01's W1 stages as contiguous 16 KiB blocks)
 hipError_t launch_pack_kstep(const bf16* in, bf16* out, int N, int K, hipStream_t st);
 hipError_t read_conv01_stamps(unsigned long long* out);  // diagnostics (VAP_CONV01_STAMPS=1)
-hipError_t read_rowpanel_stamps(unsigned long long* out);  // diagnostics (VAP_RP_STAMPS=1)
-hipError_t read_ffn_stamps(unsigned long long* out);  // diagnostics (VAP_FFN_STAMPS=1)
 hipError_t read_gemm2_stamps(unsigned long long* out);  // diagnostics (VAP_GEMM2_STAMPS=1)
 hipError_t read_lstm_stamps(unsigned long long* out);  // diagnostics (VAP_LSTM_STAMPS=1)
 
-// Row-panel GEMM (k_rowpanel.hip, bf16): C = epi(A' W^T), K = 256, N multiple of 256, rows contiguous.
-// amode 0: A bf16 rows; 1: A fp32 rows + LayerNorm(gamma, beta, eps); 2: A fp32 rows (raw -> bf16).
-// epi 0: store bf16; 1: GELU then bf16; 2: fp32 C = add + acc (add may alias C).
-struct RowPanelArgs {
-  const void* A;
-  int64_t lda;
-  int M;
-  const void* W;
-  int K, N;
-  void* C;
-  int64_t ldc;
-  const float* add;
-  const float* gamma;
-  const float* beta;
-  float eps;
-  // rows_per_seq > 0: row m = (s = m / rows_per_seq, t = m % rows_per_seq) at A + s*a_seq + t*lda,
-  // C / add + s*c_seq + t*ldc (a time chunk of every sequence); 0: rows contiguous
-  int rows_per_seq = 0;
-  int64_t a_seq = 0, c_seq = 0;
-  // w_packed: W re-laid as [N/256][K/32][16][64][8] (pack_rowpanel_weight): one k-step tile of an
-  // N tile is 16 KiB contiguous and one wave's 16-row fragment is 1 KiB contiguous in MFMA lane order
-  int w_packed = 0;
-};
-hipError_t launch_rowpanel(const RowPanelArgs& g, int amode, int epi, hipStream_t st);
-hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, int K, hipStream_t st);  // (k_misc.hip)
+// bf16 W [N][K] -> the packed projection layout [N/256][K/32][16][64][8] of the row kernels
+// (k_block.hip): one k-step of a 256-wide N tile is 16 KiB contiguous, one wave's 16-row fragment
+// 1 KiB in MFMA lane order (k_misc.hip)
+hipError_t launch_pack_rowpanel(const bf16* src, bf16* dst, int N, int K, hipStream_t st);
 
-// Fused FFN block (k_ffn.hip, bf16): x += W2 . GELU(W1 . LayerNorm(x)), x fp32 [rows][256] in place,
-// W1 [768][256] and W2 [256][768] bf16 in the PACKED projection layout (launch_pack_rowpanel with
-// K = 256 / 768).  Row addressing as RowPanelArgs (rows_per_seq / x_seq).
-struct FfnArgs {
-  float* x;
-  int M;
-  int rows_per_seq;  // 0: rows contiguous (stride 256)
-  int64_t x_seq;
-  const void* W1;
-  const void* W2;
-  const float* gamma;
-  const float* beta;
-  float eps;
-};
-hipError_t launch_ffn(const FfnArgs& g, hipStream_t st);
 // Fused layer tail (k_block.hip): x' = x + o . Wo^T (skipped when o is null), then
 // x = x' + W2 . GELU(W1 . LayerNorm(x')); weights in the packed row-panel layout.
 struct BlockArgs {

@@ -174,44 +174,9 @@ int vap_test_layernorm(int precision, const float* x, int64_t rows, const float*
   return rc_of(launch_layernorm<float>(x, rows, gamma, beta, 1e-5f, (float*)out, (float*)raw, st));
 }
 
-int vap_test_rowpanel(const void* A, int64_t lda, int M, const void* W, int K, int N, void* C, int64_t ldc,
-                      const float* add, const float* gamma, const float* beta, int amode, int epi, void* stream) {
-  RowPanelArgs g{};
-  g.A = A; g.lda = lda; g.M = M; g.W = W; g.K = K; g.N = N; g.C = C; g.ldc = ldc;
-  g.add = add; g.gamma = gamma; g.beta = beta; g.eps = 1e-5f;
-  g.w_packed = (amode & 16) != 0;  // W already in the packed row-panel layout
-  amode &= 15;
-  if ((amode == 1) != (gamma != nullptr && beta != nullptr) || (epi == 2) != (add != nullptr)) return VAP_ERR_INVALID;
-  return rc_of(launch_rowpanel(g, amode, epi, (hipStream_t)stream));
-}
-
 int vap_test_pack_weight(const void* W, void* out, int N, int K, void* stream) {
   return rc_of(launch_pack_rowpanel((const bf16*)W, (bf16*)out, N, K, (hipStream_t)stream));
 }
-int vap_test_ffn_packed(float* x, int M, const void* W1p, const void* W2p, const float* gamma, const float* beta,
-                        void* stream) {
-  FfnArgs g{x, M, 0, 0, W1p, W2p, gamma, beta, 1e-5f};
-  return rc_of(launch_ffn(g, (hipStream_t)stream));
-}
-int vap_test_ffn(float* x, int M, const void* W1, const void* W2, const float* gamma, const float* beta, void* stream) {
-  // W1 / W2 arrive in the plain [N][K] layout: pack them as the engine does at weight load
-  hipStream_t st = (hipStream_t)stream;
-  void *p1 = nullptr, *p2 = nullptr;
-  const size_t n = 768 * 256 * sizeof(bf16);
-  if (hipMalloc(&p1, n) != hipSuccess || hipMalloc(&p2, n) != hipSuccess) {
-    (void)hipFree(p1);
-    return VAP_ERR_HIP;
-  }
-  hipError_t e = launch_pack_rowpanel((const bf16*)W1, (bf16*)p1, 768, 256, st);
-  if (e == hipSuccess) e = launch_pack_rowpanel((const bf16*)W2, (bf16*)p2, 256, 768, st);
-  FfnArgs g{x, M, 0, 0, p1, p2, gamma, beta, 1e-5f};
-  if (e == hipSuccess) e = launch_ffn(g, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(p1);
-  (void)hipFree(p2);
-  return rc_of(e);
-}
-
 int vap_test_read_stamps(unsigned long long* out) { return rc_of(read_conv01_stamps(out)); }
 // fused layer tail: x = x' + FFN(LN(x')), x' = x + o . Wo^T (o may be null); plain [N][K] weights
 int vap_test_block(float* x, const void* o, int M, const void* Wo, const void* W1, const void* W2, const float* gamma,
@@ -276,10 +241,17 @@ int vap_test_lnproj(float* x, const void* o, int M, const void* Wo, const void* 
   (void)hipFree(p);
   return rc_of(e);
 }
+// the same on weights already in the packed layout (vap_test_pack_weight); no allocation, no sync
+int vap_test_lnproj_packed(float* x, const void* o, int M, const void* Wop, const void* Wpp, int np, const void* Wrp,
+                           int nr, void* cp, void* cr, const float* gamma, const float* beta, void* stream) {
+  LnProjArgs g{};
+  g.x = x; g.o = (const bf16*)o; g.M = M; g.Wo = o ? Wop : nullptr; g.Wp = Wpp; g.Wr = nr ? Wrp : nullptr;
+  g.cp = (bf16*)cp; g.ldp = np * 256; g.cr = (bf16*)cr; g.ldr = nr * 256;
+  g.gamma = gamma; g.beta = beta; g.eps = 1e-5f; g.np = np; g.nr = nr;
+  return rc_of(launch_lnproj(g, (hipStream_t)stream));
+}
 int vap_test_read_lnproj_stamps(unsigned long long* out) { return rc_of(read_lnproj_stamps(out)); }
 int vap_test_read_block_stamps(unsigned long long* out) { return rc_of(read_block_stamps(out)); }
-int vap_test_read_rp_stamps(unsigned long long* out) { return rc_of(read_rowpanel_stamps(out)); }
-int vap_test_read_ffn_stamps(unsigned long long* out) { return rc_of(read_ffn_stamps(out)); }
 int vap_test_read_gemm_stamps(unsigned long long* out) { return rc_of(read_gemm2_stamps(out)); }
 int vap_test_read_lstm_stamps(unsigned long long* out) { return rc_of(read_lstm_stamps(out)); }
 int vap_test_read_lstm_handoff(unsigned long long* out) { return rc_of(read_lstm_handoff(out)); }
