@@ -373,6 +373,211 @@ __global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// attn4: attn3's online softmax on v_mfma_f32_32x32x16_bf16.  A 16x16x32 MFMA holds the SIMD's
+// vector issue for 8 of its 16 cycles, a 32x32x16 for 8 of 32, and the kernel is bound by VALU
+// issue (exp2, max, subtract, convert per score), so the same MFMA work in half the instructions
+// leaves the softmax more issue slots.  The 32x32 layout also puts 16 keys of ONE query in a lane
+// (column = query = lane & 31, rows = keys 8(r>>2) + 4h + (r&3), h = lane >> 5): a query's max over
+// a 64-key tile is 31 lane-local max3 steps and one v_permlane32_swap (attn3: two swaps per 16 keys).
+//   S^T (64 keys x 32 queries of a wave) = K Q'^T: 2 key tiles x 4 k-steps; C starts at the key
+//     bias sl2 * key_local (one register set; the tile and 32-key offsets go into the max instead);
+//   P^T feeds O^T = V^T P^T straight from the S registers (registers 8s .. 8s+7 of a key tile are
+//     the B fragment of k-step s; its k order, keys 16s + 8(j>>2) + 4h + (j&3), is matched by the
+//     two ds_read_b64_tr_b16 reads of the V^T fragment); a ones row-block gives the denominators
+//     from the same bf16 P;
+//   K image: ds_read_b128 rows, chunk ^ ((row>>1)&7); V image: transposed reads, chunk ^ 4((row>>1)&1)
+//     (both conflict-free).
+// Dispatch, XCD-aware: the dispatcher deals workgroups to the 8 XCDs round-robin, so block b runs
+// on XCD b % 8.  When the (sequence, head) pairs divide by 8, XCD x takes the pairs p = x (mod 8),
+// in groups of `grp` pairs whose q-blocks run longest-first within the group: the K/V of the pairs
+// in flight (grp x <= 256 KiB) stay in that XCD's 4 MiB L2 instead of being fetched again for every
+// q-block (attn3 issues all pairs' longest q-blocks first, so one pair's q-blocks are far apart).
+// ------------------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+VAP_DEV f32x16 mfma32(chunk16 a, chunk16 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+VAP_DEV int vswz4(int row, int c) { return c ^ (((row >> 1) & 1) << 2); }
+VAP_DEV float xmax2(float v) {  // max with lane ^ 32
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return fmaxf(a, b);
+}
+
+__global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int grp) {
+  __shared__ __attribute__((aligned(16))) unsigned char kv[2][2][KB2 * TROW];  // [buf][K,V]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int npair = a.H * a.S;
+  int hs, qb;
+  if (grp > 0 && (npair & 7) == 0) {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, px = npair >> 3;  // pairs per XCD
+    const int g = j / (grp * nqb), r = j - g * grp * nqb;
+    const int gp = min(grp, px - g * grp);                                // pairs in this group
+    const int lv = r / gp;
+    qb = nqb - 1 - lv;
+    hs = (g * grp + (r - lv * gp)) * 8 + x;
+  } else {
+    hs = blockIdx.x % npair;
+    qb = nqb - 1 - (int)(blockIdx.x / npair);
+  }
+  const int h = hs % a.H, s = hs / a.H;
+  const int ks = a.kv_swap ? (s ^ 1) : s;
+  const bf16* Qs = (const bf16*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
+  const __amdgpu_buffer_rsrc_t rK = make_rsrc((const bf16*)a.K + (int64_t)ks * a.k_seq + h * HDIM, (uint32_t)a.T * a.k_ld * 2);
+  const __amdgpu_buffer_rsrc_t rV = make_rsrc((const bf16*)a.V + (int64_t)ks * a.v_seq + h * HDIM, (uint32_t)a.T * a.v_ld * 2);
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr float TAU = 8.0f;
+  const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
+  const int qw0 = a.q0 + qb * QB2 + w * 32;  // first query of this wave
+  const int qlast = min(a.q0 + qb * QB2 + QB2 - 1, a.T - 1);
+  const int nkb = qlast / KB2 + 1;
+  const int hl = lane >> 5, ql = lane & 31;
+  const int qv = qw0 + ql;  // this lane's query
+
+  // Q'^T fragments (B of the S MFMA): lane holds dims 16k + 8h .. +8 of its query, pre-scaled
+  chunk16 qf[4];
+  {
+    const int qc = qv < a.T ? qv : a.T - 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bf16x8 q = *(const bf16x8*)(Qs + (int64_t)qc * a.q_ld + 16 * k + 8 * hl);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = (bf16)((float)q[e] * c2);
+      qf[k] = __builtin_bit_cast(chunk16, q);
+    }
+  }
+  // key bias of the lane's S registers within a 32-key tile (the C operand of the S MFMA)
+  f32x16 kb0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) kb0[r] = sl2 * (float)(8 * (r >> 2) + 4 * hl + (r & 3));
+  const float off32 = sl2 * 32.0f, off64 = sl2 * (float)KB2;
+
+  float m = -INFINITY;  // running max of the true log2 scores
+  f32x16 o0 = {}, o1 = {}, ls = {};
+  const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
+
+  // staging (as attn3): 2 K + 2 V chunks per thread, scalar tile offset
+  const int srow = tid >> 3, sc = tid & 7;
+  const uint32_t vkoff0 = (uint32_t)(srow * a.k_ld + sc * 8) * 2, vkoff1 = vkoff0 + 32u * a.k_ld * 2;
+  const uint32_t vvoff0 = (uint32_t)(srow * a.v_ld + sc * 8) * 2, vvoff1 = vvoff0 + 32u * a.v_ld * 2;
+  const uint32_t ktile = (uint32_t)KB2 * a.k_ld * 2, vtile = (uint32_t)KB2 * a.v_ld * 2;
+  const int ldsK0 = srow * TROW + kswz2(srow, sc) * 16, ldsK1 = (srow + 32) * TROW + kswz2(srow + 32, sc) * 16;
+  const int ldsV0 = srow * TROW + vswz4(srow, sc) * 16, ldsV1 = (srow + 32) * TROW + vswz4(srow + 32, sc) * 16;
+  chunk16 rk[2], rv[2];
+  auto gload = [&](int kb) {
+    rk[0] = buf_load16(rK, vkoff0, kb * ktile);
+    rk[1] = buf_load16(rK, vkoff1, kb * ktile);
+    rv[0] = buf_load16(rV, vvoff0, kb * vtile);
+    rv[1] = buf_load16(rV, vvoff1, kb * vtile);
+  };
+  auto lstore = [&](int buf) {
+    *(chunk16*)(kv[buf][0] + ldsK0) = rk[0];
+    *(chunk16*)(kv[buf][0] + ldsK1) = rk[1];
+    *(chunk16*)(kv[buf][1] + ldsV0) = rv[0];
+    *(chunk16*)(kv[buf][1] + ldsV1) = rv[1];
+  };
+  // K fragment of key tile t, k-step k: row 32t + ql, chunk 2k + hl (the 32t part is an immediate)
+  int koff[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) koff[k] = ql * TROW + kswz2(ql, 2 * k + hl) * 16;
+  // V^T fragment, dims 32u + ql, keys 32t + 16s + 4hl + {0..3} (+8 for elements 4..7): the lane
+  // supplies row 4hl + q, columns 32u + 16(g&1) + 4p of its 16-lane group g (lane = 16g + 4q + p)
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
+  int voff[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    voff[u] = (4 * hl + tq) * TROW + vswz4(4 * hl + tq, 4 * u + 2 * tg + (tp >> 1)) * 16 + (tp & 1) * 8;
+
+  auto tile = [&](int kb, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    if (kb + 1 < nkb) gload(kb + 1);
+    const int key0 = kb * KB2;
+    if (key0 <= qw0 + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
+      const unsigned char* Kt = kv[cur][0];
+      const unsigned char* Vt = kv[cur][1];
+      f32x16 st[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        st[t] = kb0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st[t] = mfma32(*(const chunk16*)(Kt + t * 32 * TROW + koff[k]), qf[k], st[t]);
+      }
+      if (key0 + KB2 - 1 > qw0) {  // wave-uniform: a diagonal tile
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (key0 + 32 * t + 8 * (r >> 2) + 4 * hl + (r & 3) > qv) st[t][r] = -INFINITY;
+      }
+      float b0 = st[0][0], b1 = st[1][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        b0 = fmaxf(b0, st[0][r]);
+        b1 = fmaxf(b1, st[1][r]);
+      }
+      const float tofs = off64 * (float)kb;
+      const float bm = xmax2(fmaxf(b0, b1 + off32)) + tofs;  // the tile's max true score of the lane's query
+      if (__ballot(bm > m + TAU)) {  // wave-uniform: raise the running max, rescale O and the sums
+        const float mn = fmaxf(m, bm);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+        o0 *= alpha;
+        o1 *= alpha;
+        ls *= alpha;
+      }
+      const float m0 = m - tofs, m1 = m0 - off32;
+      bf16x8 pb[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const float mt = t ? m1 : m0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pb[t][k][e] = (bf16)__builtin_amdgcn_exp2f(st[t][8 * k + e] - mt);
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const chunk16 p = __builtin_bit_cast(chunk16, pb[t][k]);
+          const int ro = (32 * t + 16 * k) * TROW;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const u32x2 v0 = tr_read(Vt + ro + voff[u]);
+            const u32x2 v1 = tr_read(Vt + ro + 8 * TROW + voff[u]);
+            const chunk16 vf = {v0.x, v0.y, v1.x, v1.y};
+            if (u == 0) o0 = mfma32(vf, p, o0);
+            else o1 = mfma32(vf, p, o1);
+          }
+          ls = mfma32(ones, p, ls);
+        }
+    }
+    if (kb + 1 < nkb) lstore(cur ^ 1);
+    __syncthreads();
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; kb += 2) {  // unrolled by 2: the LDS buffer index is a constant
+    tile(kb, std::integral_constant<int, 0>{});
+    if (kb + 1 < nkb) tile(kb + 1, std::integral_constant<int, 1>{});
+  }
+  // O^T: lane holds its query's dims 32u + 8g + 4hl + e in register 4g + e of o_u
+  const float inv = 1.0f / ls[0];
+  if (qv < a.T) {
+    bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv * a.o_ld + h * HDIM;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      store4(orow + 8 * g + 4 * hl, o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+      store4(orow + 32 + 8 * g + 4 * hl, o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    }
+  }
+}
+
 }  // namespace
 
 template <typename T>
@@ -381,7 +586,10 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
     const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
-    hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
+    static const int ver = getenv("VAP_ATTN3") ? 3 : 4;        // A/B: the 16x16x32 kernel
+    static const int grp = getenv("VAP_ATTN_GRP") ? atoi(getenv("VAP_ATTN_GRP")) : 8;
+    if (ver == 3) hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
+    else hipLaunchKernelGGL(attn4_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
     return hipGetLastError();
   }
   if (a.q0 != 0) return hipErrorInvalidValue;

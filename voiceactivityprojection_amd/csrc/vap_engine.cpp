@@ -312,13 +312,13 @@ Plan make_plan(int B, int64_t N, size_t es, int kv_self_layers = 0, int kv_cross
   p.H1 = take(S * p.sh * es);
   p.X = take(S * T * D * sizeof(float));
   // bf16 mode: LayerNorm, FFN hidden and combinator rows stay on chip (fused row kernels of
-  // k_block.hip), so LN / FF / HC / HCT are fp32-mode buffers; the time-chunked schedule keeps Q/K/V
-  // per layer (QKVL / KVCL) instead of QKV / KVC
-  const bool fp = es == 4, tc = kv_self_layers > 0;
+  // k_block.hip), so LN / FF / HC / HCT are fp32-mode buffers.  QKV / KVC stay in a time-chunked
+  // plan too (its QKVL / KVCL hold every layer's): attention=True and encode run the serial schedule
+  const bool fp = es == 4;
   p.LN = take(fp ? S * T * D * es : 0);
   p.RAW = take(S * T * D * es);
-  p.QKV = take(tc ? 0 : S * T * 3 * D * es);
-  p.KVC = take(tc ? 0 : S * T * 2 * D * es);
+  p.QKV = take(S * T * 3 * D * es);
+  p.KVC = take(S * T * 2 * D * es);
   p.QC = take(S * T * D * es);
   p.ATT = take(S * T * D * es);
   p.FF = take(fp ? S * T * 3 * D * es : 0);
