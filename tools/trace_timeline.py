@@ -9,7 +9,7 @@ import sys
 
 
 def short(n):
-    for k in ("lstm_pair", "lstm_resident", "conv01", "gemm2_kernelIDF16b", "gemm2_kernel<float", "attn3", "block_kernel",
+    for k in ("lstm_pair", "lstm_resident", "conv01", "convk4", "gemm2_kernelIDF16b", "gemm2_kernel<float", "attn4", "attn3", "block_kernel", "block3", "heads_kernel",
               "lnproj_kernel", "rowpanel", "streamOpsWait", "streamOpsWrite", "probs", "labels", "vad_head",
               "zero_rows", "copyBuffer", "layernorm"):
         if k in n:

@@ -175,214 +175,19 @@ VAP_DEV u32x2 tr_read(const unsigned char* p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// attn3: that tiling with the softmax VALU cut down (the kernel is VALU-bound at head_dim 64:
-// ~256 MFMA FLOPs but ~6 VALU ops per score):
-//  * the query term of the AliBi bias cancels in the softmax, so v = s*c2 + sl2*key: one FMA per
-//    score against a per-tile key-bias vector (16 registers, one add per 2 scores per tile);
-//  * lazy rescaling: the running max m is only raised (and O, l rescaled) when a tile's max
-//    exceeds it by more than 8 (log2 domain), decided wave-uniformly; otherwise exp2(v - m) <= 256
-//    is exact enough for the bf16 P operand and the fp32 sums;
-//  * longest-first dispatch: the causal q-blocks with the most key tiles start first, so the tail
-//    of the grid is made of the short ones.
-// ------------------------------------------------------------------------------------------
-// V tile swizzle for the transpose reads: each 32-lane half reads 8 rows (4 per row parity) x four
-// 8-byte pieces of one 32-byte column band; XOR-ing the 16-byte chunk with 2*((row>>1)&3) spreads
-// the same-parity rows over the 256-byte bank row (4-way conflicted without it).
-VAP_DEV int vswz3(int row, int c) { return c ^ (((row >> 1) & 3) << 1); }
-// max over the four 16-lane groups (lanes l, l^16, l^32, l^48) by permlane swaps: no LDS round trip
-// and no bpermute address math (inline asm: the builtins given equal operands are miscompiled)
-VAP_DEV float xmax4(float v) {
-  float a = v, b = v;
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-  float c = fmaxf(a, b), d = c;
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));
-  return fmaxf(c, d);
-}
-
-__global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
-  __shared__ __attribute__((aligned(16))) unsigned char kv[2][2][KB2 * TROW];  // [buf][K,V]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int hs = blockIdx.x % (a.H * a.S);
-  const int qb = nqb - 1 - (int)(blockIdx.x / (a.H * a.S));
-  const int h = hs % a.H, s = hs / a.H;
-  const int ks = a.kv_swap ? (s ^ 1) : s;
-  const bf16* Qs = (const bf16*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
-  // K / V rows of this (sequence, head) through buffer resources: rows >= T read as zeros
-  const __amdgpu_buffer_rsrc_t rK = make_rsrc((const bf16*)a.K + (int64_t)ks * a.k_seq + h * HDIM, (uint32_t)a.T * a.k_ld * 2);
-  const __amdgpu_buffer_rsrc_t rV = make_rsrc((const bf16*)a.V + (int64_t)ks * a.v_seq + h * HDIM, (uint32_t)a.T * a.v_ld * 2);
-  constexpr float LOG2E = 1.4426950408889634f;
-  constexpr float TAU = 8.0f;
-  const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
-  const int qw0 = a.q0 + qb * QB2 + w * 32;  // first query of this wave (absolute)
-  const int qlast = min(a.q0 + qb * QB2 + QB2 - 1, a.T - 1);
-  const int nkb = qlast / KB2 + 1;
-
-  chunk16 qf[2][2];
-  int qv[2];
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
-    qv[qs] = qw0 + qs * 16 + (lane & 15);
-    const int qc = qv[qs] < a.T ? qv[qs] : a.T - 1;
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
-      // Q pre-scaled by scale*log2(e) once per workgroup: the S MFMA then yields log2-domain scores
-      bf16x8 q = *(const bf16x8*)(Qs + (int64_t)qc * a.q_ld + (kg * 4 + (lane >> 4)) * 8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = (bf16)((float)q[e] * c2);
-      qf[qs][kg] = __builtin_bit_cast(chunk16, q);
-    }
-  }
-  // key bias sl2*key of the lane's score registers (the S MFMA's C operand), + sl2*KB2 per tile
-  f32x4 kb4[4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kb4[kt][r] = sl2 * (float)(kt * 16 + (lane >> 4) * 4 + r);
-  const float kstep = sl2 * (float)KB2;
-
-  // o[qs][0..3]: O^T d-tiles; o[qs][4]: a ones row-block of V^T, i.e. the softmax denominators
-  // accumulated by the MFMA from the same bf16 P that forms the numerator
-  float m[2] = {-INFINITY, -INFINITY};
-  f32x4 o[2][5];
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-    for (int dt = 0; dt < 5; ++dt) o[qs][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
-  const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
-
-  // staging: K and V tiles are 512 chunks each, 2 + 2 per thread; per-thread byte offsets are
-  // fixed, the tile offset is scalar
-  const int srow = tid >> 3, sc = tid & 7;
-  const uint32_t vkoff0 = (uint32_t)(srow * a.k_ld + sc * 8) * 2, vkoff1 = vkoff0 + 32u * a.k_ld * 2;
-  const uint32_t vvoff0 = (uint32_t)(srow * a.v_ld + sc * 8) * 2, vvoff1 = vvoff0 + 32u * a.v_ld * 2;
-  const uint32_t ktile = (uint32_t)KB2 * a.k_ld * 2, vtile = (uint32_t)KB2 * a.v_ld * 2;
-  const int ldsK0 = srow * TROW + kswz2(srow, sc) * 16, ldsK1 = (srow + 32) * TROW + kswz2(srow + 32, sc) * 16;
-  const int ldsV0 = srow * TROW + vswz3(srow, sc) * 16, ldsV1 = (srow + 32) * TROW + vswz3(srow + 32, sc) * 16;
-  chunk16 rk[2], rv[2];
-  auto gload = [&](int kb) {
-    rk[0] = buf_load16(rK, vkoff0, kb * ktile);
-    rk[1] = buf_load16(rK, vkoff1, kb * ktile);
-    rv[0] = buf_load16(rV, vvoff0, kb * vtile);
-    rv[1] = buf_load16(rV, vvoff1, kb * vtile);
-  };
-  auto lstore = [&](int buf) {
-    *(chunk16*)(kv[buf][0] + ldsK0) = rk[0];
-    *(chunk16*)(kv[buf][0] + ldsK1) = rk[1];
-    *(chunk16*)(kv[buf][1] + ldsV0) = rv[0];
-    *(chunk16*)(kv[buf][1] + ldsV1) = rv[1];
-  };
-  // per-lane LDS read offsets (the tile buffer adds a compile-time constant)
-  // (kswz2 does not depend on the 16-row sub-tile, vswz3 not on the 32-row half: those parts are
-  // immediate offsets)
-  const int krow = lane & 15;
-  const int koff0 = krow * TROW + kswz2(krow, lane >> 4) * 16, koff1 = krow * TROW + kswz2(krow, 4 + (lane >> 4)) * 16;
-  const int qq = (lane & 15) >> 2, pp = lane & 3;
-  const int r0 = (lane >> 4) * 4 + qq;  // rows r0 (+16, +32, +48) share vswz3
-  int voff[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) voff[dt] = r0 * TROW + vswz3(r0, dt * 2 + (pp >> 1)) * 16 + (pp & 1) * 8;
-
-  auto tile = [&](int kb, auto cur_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    if (kb + 1 < nkb) gload(kb + 1);
-    const int key0 = kb * KB2;
-    if (key0 <= qw0 + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
-      const unsigned char* Kt = kv[cur][0];
-      const unsigned char* Vt = kv[cur][1];
-      f32x4 st[2][4];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const chunk16 k0 = *(const chunk16*)(Kt + kt * 16 * TROW + koff0);
-        const chunk16 k1 = *(const chunk16*)(Kt + kt * 16 * TROW + koff1);
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs) st[qs][kt] = mfma_chunk<bf16>(k1, qf[qs][1], mfma_chunk<bf16>(k0, qf[qs][0], kb4[kt]));
-      }
-      if (key0 + KB2 - 1 > qw0) {  // wave-uniform: a diagonal tile, some key lies above some query
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (key0 + kt * 16 + (lane >> 4) * 4 + r > qv[qs]) st[qs][kt][r] = -INFINITY;
-      }
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        float bm = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-          bm = fmaxf(bm, fmaxf(fmaxf(st[qs][kt][0], st[qs][kt][1]), fmaxf(st[qs][kt][2], st[qs][kt][3])));
-        bm = xmax4(bm);
-        if (__ballot(bm > m[qs] + TAU)) {  // wave-uniform: raise the running max, rescale O and l
-          const float mn = fmaxf(m[qs], bm);
-          const float alpha = __builtin_amdgcn_exp2f(m[qs] - mn);
-          m[qs] = mn;
-#pragma unroll
-          for (int dt = 0; dt < 5; ++dt) o[qs][dt] *= alpha;
-        }
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) st[qs][kt][r] = __builtin_amdgcn_exp2f(st[qs][kt][r] - m[qs]);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 pb[2];
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs)
-          pb[qs] = bf16x8{(bf16)st[qs][2 * kk][0], (bf16)st[qs][2 * kk][1], (bf16)st[qs][2 * kk][2],
-                          (bf16)st[qs][2 * kk][3], (bf16)st[qs][2 * kk + 1][0], (bf16)st[qs][2 * kk + 1][1],
-                          (bf16)st[qs][2 * kk + 1][2], (bf16)st[qs][2 * kk + 1][3]};
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const u32x2 v0 = tr_read(Vt + kk * 32 * TROW + voff[dt]);
-          const u32x2 v1 = tr_read(Vt + kk * 32 * TROW + 16 * TROW + voff[dt]);
-          const chunk16 af = {v0.x, v0.y, v1.x, v1.y};
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs) o[qs][dt] = mfma_chunk<bf16>(af, __builtin_bit_cast(chunk16, pb[qs]), o[qs][dt]);
-        }
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs) o[qs][4] = mfma_chunk<bf16>(ones, __builtin_bit_cast(chunk16, pb[qs]), o[qs][4]);
-      }
-    }
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) kb4[kt] += kstep;
-    if (kb + 1 < nkb) lstore(cur ^ 1);
-    __syncthreads();
-  };
-
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kb = 0; kb < nkb; kb += 2) {  // unrolled by 2: the LDS buffer index is a constant
-    tile(kb, std::integral_constant<int, 0>{});
-    if (kb + 1 < nkb) tile(kb + 1, std::integral_constant<int, 1>{});
-  }
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
-    const float inv = 1.0f / o[qs][4][0];
-    if (qv[qs] < a.T) {
-      bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv[qs] * a.o_ld + h * HDIM;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + (lane >> 4) * 4;
-        store4(orow + d, o[qs][dt][0] * inv, o[qs][dt][1] * inv, o[qs][dt][2] * inv, o[qs][dt][3] * inv);
-      }
-    }
-  }
-}
-
-
-// ------------------------------------------------------------------------------------------
-// attn4: attn3's online softmax on v_mfma_f32_32x32x16_bf16.  A 16x16x32 MFMA holds the SIMD's
-// vector issue for 8 of its 16 cycles, a 32x32x16 for 8 of 32, and the kernel is bound by VALU
-// issue (exp2, max, subtract, convert per score), so the same MFMA work in half the instructions
-// leaves the softmax more issue slots.  The 32x32 layout also puts 16 keys of ONE query in a lane
-// (column = query = lane & 31, rows = keys 8(r>>2) + 4h + (r&3), h = lane >> 5): a query's max over
-// a 64-key tile is 31 lane-local max3 steps and one v_permlane32_swap (attn3: two swaps per 16 keys).
-//   S^T (64 keys x 32 queries of a wave) = K Q'^T: 2 key tiles x 4 k-steps; C starts at the key
-//     bias sl2 * key_local (one register set; the tile and 32-key offsets go into the max instead);
+// attn4: the bf16 kernel.  Online softmax in the exp2 domain with the softmax VALU cut down (the
+// kernel is VALU- and latency-bound at head_dim 64: ~256 MFMA FLOPs but ~4 VALU ops per score):
+//  * the query term of the AliBi bias cancels in the softmax, so the score is s*c2 + sl2*key: the
+//    S MFMA's C operand starts at the key bias of a 32-key tile (one register set); the tile and
+//    32-key offsets go into the running max instead of the scores;
+//  * lazy rescaling: the running max m is only raised (and O, l rescaled) when a tile's max exceeds
+//    it by more than 8 (log2 domain), decided wave-uniformly; otherwise exp2(v - m) <= 256 is exact
+//    enough for the bf16 P operand and the fp32 sums;
+//  * v_mfma_f32_32x32x16_bf16 throughout (a 16x16x32 MFMA holds the SIMD's vector issue for 8 of its
+//    16 cycles, a 32x32x16 for 8 of 32); the 32x32 layout puts 16 keys of ONE query in a lane
+//    (column = query = lane & 31, rows = keys 8(r>>2) + 4h + (r&3), h = lane >> 5), so a query's max
+//    over a 64-key tile is lane-local max3 steps and one v_permlane32_swap.
+//   S^T (64 keys x 32 queries of a wave) = K Q'^T: 2 key tiles x 4 k-steps;
 //   P^T feeds O^T = V^T P^T straight from the S registers (registers 8s .. 8s+7 of a key tile are
 //     the B fragment of k-step s; its k order, keys 16s + 8(j>>2) + 4h + (j&3), is matched by the
 //     two ds_read_b64_tr_b16 reads of the V^T fragment); a ones row-block gives the denominators
@@ -393,7 +198,10 @@ __global__ __launch_bounds__(256, 3) void attn3_kernel(AttnArgs a, int nqb) {
 // on XCD b % 8.  When the (sequence, head) pairs divide by 8, XCD x takes the pairs p = x (mod 8),
 // in groups of `grp` pairs whose q-blocks run longest-first within the group: the K/V of the pairs
 // in flight (grp x <= 256 KiB) stay in that XCD's 4 MiB L2 instead of being fetched again for every
-// q-block (attn3 issues all pairs' longest q-blocks first, so one pair's q-blocks are far apart).
+// q-block (FETCH_SIZE 319 -> 96 MB per 128-sequence launch; a longest-first order over all pairs
+// puts one pair's q-blocks far apart in time).
+// Measured and dropped: K / V tiles by LDS-DMA into a 3-slot ring two tiles ahead with the K
+// fragments of a 32-key half read together (no faster: 149 vs 149 us per 128 x 1000 launch).
 // ------------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VAP_DEV f32x16 mfma32(chunk16 a, chunk16 b, f32x16 c) {
@@ -459,7 +267,7 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
   const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
 
-  // staging (as attn3): 2 K + 2 V chunks per thread, scalar tile offset
+  // staging: 2 K + 2 V chunks per thread, scalar tile offset
   const int srow = tid >> 3, sc = tid & 7;
   const uint32_t vkoff0 = (uint32_t)(srow * a.k_ld + sc * 8) * 2, vkoff1 = vkoff0 + 32u * a.k_ld * 2;
   const uint32_t vvoff0 = (uint32_t)(srow * a.v_ld + sc * 8) * 2, vvoff1 = vvoff0 + 32u * a.v_ld * 2;
@@ -578,6 +386,7 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
   }
 }
 
+
 }  // namespace
 
 template <typename T>
@@ -586,10 +395,8 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
     if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
     const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
-    static const int ver = getenv("VAP_ATTN3") ? 3 : 4;        // A/B: the 16x16x32 kernel
-    static const int grp = getenv("VAP_ATTN_GRP") ? atoi(getenv("VAP_ATTN_GRP")) : 8;
-    if (ver == 3) hipLaunchKernelGGL(attn3_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb);
-    else hipLaunchKernelGGL(attn4_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
+    constexpr int grp = 8;  // (sequence, head) pairs per XCD group: K/V of 8 pairs x <= 256 KiB in L2
+    hipLaunchKernelGGL(attn4_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
     return hipGetLastError();
   }
   if (a.q0 != 0) return hipErrorInvalidValue;
