@@ -239,6 +239,13 @@ def run_rank(args) -> int:
         # gated by) the front / back ends, so its launch time is mostly waiting, not work
         # (single-kernel classes only: tr_gemm / heads mix several kernels)
         dominant = max(("conv1", "conv234", "lstm_proj", "downsample", "attn"), key=breakdown.get)
+        # the same class with the front end on ONE stream (one untimed forward): the kernel's own
+        # duration, not shared with conv2..4 of the previous piece on the second front-end stream
+        N.check(lib.vap_timing(h, -N.KERNEL_CLASS[dominant]))
+        model.probs(wav, out=packs[0].views())
+        iso_tot, iso_cnt = ctypes.c_double(), ctypes.c_int()
+        N.check(lib.vap_timing_read(h, ctypes.byref(iso_tot), ctypes.byref(iso_cnt)))
+        model.synchronize()
         N.check(lib.vap_timing(h, N.KERNEL_CLASS[dominant]))
 
     # timed region: K steps (+ their gathers), HIP events around every launch of the dominant class
@@ -317,11 +324,21 @@ def run_rank(args) -> int:
                                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                                 "traffic_source": traffic_src, "flop_per_launch": flop_per_launch,
                                 "ms_per_launch": round(dom_ms_per_launch, 4), "launches": cnt.value}
+            if dominant in ("conv1", "conv234", "lstm_proj"):
+                iso_ms = iso_tot.value / max(1, iso_cnt.value)
+                iso_ach = flop_per_launch / (iso_ms * 1e-3) / 1e12
+                line["roofline"]["concurrency"] = (
+                    "timed region: the front end runs on two streams, so each launch shares the CUs with conv2..4 "
+                    "and the gate projection of the previous piece (ms_per_launch is that shared duration); "
+                    "isolated: the same launches with the front end on one stream (one untimed forward)")
+                line["roofline"]["isolated"] = {"ms_per_launch": round(iso_ms, 4), "achieved": round(iso_ach, 2),
+                                                "frac": round(iso_ach / peak, 4)}
             line["breakdown_ms_per_step"] = breakdown
             line["breakdown_note"] = ("ms of each kernel class per step (HIP events on its stream); lstm_rec is one "
                                       "persistent side-stream launch overlapped with the caller-stream classes (its "
-                                      "time includes waiting for the time chunks), the other classes run back to "
-                                      "back on the caller's stream")
+                                      "time includes waiting for the time chunks); the front end runs on two "
+                                      "streams (conv01 of piece k+1 beside conv2..4 + gate projection of piece k), "
+                                      "the back end back to back on the caller's stream")
             line["model_tflops_per_s"] = round(sum(flops.values()) * args.steps * world / el / 1e12, 2)
         if world == 1 and not args.no_cpu_baseline and not args.stub:
             line["cpu_baseline"] = cpu_baseline(args.seconds, sd_np)

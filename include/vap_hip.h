@@ -168,7 +168,8 @@ int vap_labels_loss(const float* logits, const float* va, int batch, int frames,
  * vap_stream_push on the handle (a host read of a mapped word, no device sync). */
 int vap_synchronize(vap_handle* h, void* stream);
 
-/* Timing hook: record HIP events around every launch of kernel class `cls` (0 = off). */
+/* Timing hook: record HIP events around every launch of kernel class `cls` (0 = off); -cls times
+ * the class with the time-pipelined front end on the caller stream only (no second stream). */
 int vap_timing(vap_handle* h, int cls);
 /* Synchronises the recorded events; total device milliseconds and launch count since last read. */
 int vap_timing_read(vap_handle* h, double* total_ms, int* launches);

@@ -72,7 +72,7 @@ struct vap_handle {
   // (VAP_FE_STREAMS=2, session 4: within 1 % of one stream in the bench, +1.5 % in back-to-back
   // forwards without per-launch timing events; one stream keeps each kernel's events clean)
   hipStream_t fe_stream = nullptr;
-  int fe_streams = 1;
+  int fe_streams = 2;
   bool fe_first_serial = false;
   int fe_gate = 0;  // VAP_FE_GATE: see conv_rows
   bool fe_align = true;  // VAP_FE_ALIGN=0: conv1..3 ranges per piece exactly what its conv4 rows need
@@ -148,6 +148,7 @@ struct vap_handle {
   }
   // timing hook
   int timing_cls = 0;
+  bool timing_serial = false;  // vap_timing(h, -cls): the front end on the caller stream only
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
 
@@ -1399,8 +1400,10 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
   int64_t done_rows = 0, done_lv[3] = {0, 0, 0};
   int published = 0;
   // conv2..4 + gate projections (and the ready flags) on the front-end stream, conv01 on st
-  // (timing mode, vap_timing: one stream, so each class's events bracket only its own kernels)
-  hipStream_t fst = h->fe_streams < 2 || h->timing_cls ? nullptr
+  // (timing mode, vap_timing, for a class that would run on the front-end stream: one stream, so its
+  // events bracket only its own kernels; the bench times conv1, whose launches stay on st)
+  const bool fe_timed = h->timing_serial || h->timing_cls == VAP_K_CONV234 || h->timing_cls == VAP_K_LSTM_PROJ;
+  hipStream_t fst = h->fe_streams < 2 || fe_timed ? nullptr
                     : h->fe_stream                   ? h->fe_stream
                     : h->tc_streams < 2              ? h->side[1]
                                                      : nullptr;
@@ -2216,7 +2219,8 @@ int vap_test_xtag(vap_handle* h, int64_t set, int64_t* get) {
 
 int vap_timing(vap_handle* h, int cls) {
   if (!h) return fail(VAP_ERR_INVALID, "null handle");
-  h->timing_cls = cls;
+  h->timing_serial = cls < 0;
+  h->timing_cls = cls < 0 ? -cls : cls;
   h->ev_used = 0;
   return VAP_OK;
 }
