@@ -117,6 +117,19 @@ def test_heads_per_chunk_equals_once(monkeypatch):
         assert torch.equal(out[k], ref[k]), k
 
 
+def test_block_fused_projections_equal_separate(monkeypatch):
+    """In the time-chunked back end each layer's block kernel also computes the next layer's
+    LayerNorm'd Q/K/V and raw-row cross K/V (k_block.hip, BlockArgs.np); VAP_BLOCK_FUSE=0 runs the
+    separate lnproj launches.  Same LayerNorm, same bf16 rounding, same k-step order: bit-identical."""
+    w = _batch(3, 320000, 901)
+    monkeypatch.setenv("VAP_BLOCK_FUSE", "0")
+    ref = _model().probs(w)
+    monkeypatch.setenv("VAP_BLOCK_FUSE", "1")
+    out = _model().probs(w)
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
+
+
 def test_bf16_repeat_determinism_and_xcd_handshake():
     """Repeated forwards are bit-identical (the pair recurrence's exchange protocol and the
     hand-counted vmcnt waits leave no race), and the XCD handshake of the last pair launch keeps

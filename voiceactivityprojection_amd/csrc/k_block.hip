@@ -146,12 +146,13 @@ VAP_DEV void ln_panel(const f32x4 (&acc)[2][MT], float* red0, float* red1, const
 // issued, [17] stores complete
 __device__ unsigned long long g_blk_stamps[8][24];
 
-template <int MT, bool OPROJ, bool ST = false, int NPF = 2>
+template <int MT, bool OPROJ, bool ST = false, int NPF = 2, int NP2 = 0, int NR2 = 0>
 __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   using C = Blk<MT>;
   constexpr int R = C::R;
   constexpr int Q0 = OPROJ ? 8 : 0;      // first FFN k-step of the weight stream
-  constexpr int NQ = Q0 + 48;            // Wo 8 + 3 x (W1 8 + W2 8)
+  constexpr int Q2 = Q0 + 48;            // first k-step of the fused next-layer projections
+  constexpr int NQ = Q2 + 8 * (NP2 + NR2);  // Wo 8 + 3 x (W1 8 + W2 8) [+ Wp / Wr 8 per N tile]
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
   unsigned char* P = smem;
   unsigned char* H = smem + C::OFF_H;
@@ -231,14 +232,19 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     int kidx;
     const bool o = OPROJ && q < Q0;
     bool second = false;
+    __amdgpu_buffer_rsrc_t rs;
     if (o) {
       kidx = q;
-    } else {
+      rs = rWo;
+    } else if (q < Q2) {
       const int t = q - Q0, s = t >> 4, u = t & 15;
       second = u >= 8;
       kidx = s * 8 + (u & 7);
+      rs = second ? rW2 : rW1;
+    } else {  // fused next-layer projection tiles (Wp then Wr, back to back)
+      kidx = q - Q2;
+      rs = make_rsrc(g.Wp, 0x7FFFFFF0u);
     }
-    const __amdgpu_buffer_rsrc_t rs = o ? rWo : second ? rW2 : rW1;
 #pragma unroll
     for (int i = 0; i < 2; ++i) r[i] = buf_load16(rs, wlo, (uint32_t)((kidx * 16 + 2 * w + i) * 1024));
   };
@@ -349,6 +355,78 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
                      pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
     }
   }
+  if constexpr (NP2 > 0) {
+    // ---------------------------------------------------------------- next layer: LN2(x) -> Q/K/V, x -> cross K/V
+    // (the rows are already in the accumulators: no re-read of x, one launch less; modules.py:252-272)
+    // lane-derived offsets rebuilt from an opaque zero: reusing the prologue's keeps them live
+    // through the FFN (+20 VGPRs, half the occupancy)
+    int z2;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z2));
+    const int tidb = tid + z2, l16b = l16 + z2, lgb = lg + z2;
+    // this phase's arguments read here from the kernel-argument segment through an opaque pointer: held
+    // from the prologue they spill SGPRs into a VGPR
+    using KA = const __attribute__((address_space(4))) BlockArgs*;
+    KA ka = (KA)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    f32x4 gb2 = {0.f, 0.f, 0.f, 0.f};
+    if (tidb < 128) gb2 = *(const f32x4*)((tidb < 64 ? ka->gamma2 : ka->beta2) + (tidb & 63) * 4);
+    __syncthreads();  // every wave is done with P (slice 2's up), H (slice 2's down) and GB (the first LN)
+    if (tidb < 128) *(f32x4*)(GB + tidb * 4) = gb2;
+    if constexpr (NR2 > 0) {  // raw rows (bf16) -> H
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n = w * 32 + i * 16 + lgb * 4;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+          const int row = j * 16 + l16b;
+          *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
+              pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ln_panel<MT>(acc, red0, red1, GB, P, w, l16b, lgb, g.eps);
+    __syncthreads();  // P (and the raw panel) complete
+    __builtin_amdgcn_sched_barrier(0);
+    auto roffl = [&](int m, int64_t seq, int64_t ld) -> int64_t {
+      if (g.rows_per_seq == 0) return (int64_t)m * ld;
+      const int sq = m / g.rows_per_seq;
+      return (int64_t)sq * seq + (int64_t)(m - sq * g.rows_per_seq) * ld;
+    };
+#pragma unroll
+    for (int p = 0; p < NP2 + NR2; ++p) {
+      const bool raw = p >= NP2;
+      const int nt = raw ? p - NP2 : p;
+      f32x4 c[2][MT];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) c[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) kstep(raw ? H : P, ks, Q2 + 8 * p + ks, c);
+      bf16* out = raw ? ka->cr : ka->cp;
+      const int wd = raw ? NR2 : NP2;  // output row width in 256-wide tiles
+      const int64_t ld = (int64_t)wd * D, seq = g.x_seq * wd;
+      const int64_t cbase = roffl(m0, seq, ld);
+      const __amdgpu_buffer_rsrc_t rc = make_rsrc(out + cbase, 0x7FFFFFF0u);
+      uint32_t co[MT];
+      rows16_off(m0 + l16b, g.M, g.rows_per_seq, seq, ld, cbase, 2, co, MT);
+      const uint32_t col = (uint32_t)(nt * 256 + w * 32 + (lgb & 1) * 16 + (lgb >> 1) * 8);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        u32x2 a = pack_bf16x4(c[0][j][0], c[0][j][1], c[0][j][2], c[0][j][3]);
+        u32x2 b = pack_bf16x4(c[1][j][0], c[1][j][1], c[1][j][2], c[1][j][3]);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(a[d], b[d], false, false);
+          a[d] = sw[0];
+          b[d] = sw[1];
+        }
+        buf_store16(rc, co[j] + col * 2u, u32x4{a[0], a[1], b[0], b[1]});
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   if constexpr (ST) {
     stamp(16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -363,6 +441,14 @@ hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
   static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
   static const int npf = getenv("VAP_BLOCK_NPF") ? atoi(getenv("VAP_BLOCK_NPF")) : 2;
+  if (g.np) {  // fused next-layer projections (the 64-row variant only: launch_block forces MT 4)
+    if constexpr (MT == 4) {
+      if (g.nr) hipLaunchKernelGGL((block_kernel<MT, true, false, 2, 3, 2>), grid, dim3(512), 0, st, g);
+      else hipLaunchKernelGGL((block_kernel<MT, true, false, 2, 3, 0>), grid, dim3(512), 0, st, g);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (stamps && g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, true, 8>), grid, dim3(512), 0, st, g);
   else if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
   else if (g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, false, 8>), grid, dim3(512), 0, st, g);
@@ -380,12 +466,20 @@ hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
 // 64-row workgroups would not cover in one round
 hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st) {
   if (g.M <= 0 || g.rows_per_seq < 0 || !g.x || !g.W1 || !g.W2 || (g.o && !g.Wo)) return hipErrorInvalidValue;
+  if (g.np && (g.np != 3 || (g.nr != 0 && g.nr != 2) || !g.o || !g.Wp || !g.cp || !g.gamma2 || !g.beta2 ||
+               (g.nr && !g.cr)))
+    return hipErrorInvalidValue;
   static const int force = getenv("VAP_BLOCK_MT") ? atoi(getenv("VAP_BLOCK_MT")) : 0;
-  const int mt = force ? force : (cus > 0 && cus < 64 && (g.M + 63) / 64 > 2 * cus ? 9 : 4);
+  const int mt = g.np ? 4 : force ? force : (cus > 0 && cus < 64 && (g.M + 63) / 64 > 2 * cus ? 9 : 4);
   const int bm = 16 * mt;
   // a panel's rows must lie within the 2 GiB a buffer offset reaches from its first row
   const int64_t span = g.rows_per_seq ? (bm / g.rows_per_seq + 2) * g.x_seq + (int64_t)bm * D : (int64_t)bm * D;
   if (span * 4 >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+  auto span2 = [&](int64_t seq, int64_t ld) {
+    return (g.rows_per_seq ? (bm / g.rows_per_seq + 2) * seq + (int64_t)bm * ld : (int64_t)bm * ld) * 2;
+  };
+  if (g.np && span2(g.x_seq * 3, 3 * D) >= 0x7FFFFFF0LL)
+    return hipErrorInvalidValue;
   if (mt == 4) return launch_mt<4>(g, st);
   if (mt == 9) return launch_mt<9>(g, st);
   return hipErrorInvalidValue;

@@ -91,6 +91,10 @@ struct vap_handle {
   // bf16 recurrence: split over workgroup pairs (k_lstm.hip lstm_pair_kernel, two CUs per 16 sequences)
   // conv2..4 on the slab-staged k4 s2 kernel (k_conv234.hip); VAP_CONVK4=0: implicit GEMMs on gemm2
   bool convk4 = true;
+  // time-chunked back end: each layer's block kernel also computes the next layer's LN + Q/K/V (and
+  // cross K/V) from the rows it holds, one launch and one read of x less per layer transition
+  // (VAP_BLOCK_FUSE=0: separate lnproj launches)
+  bool block_fuse = true;
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
   // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
@@ -552,6 +556,12 @@ int pack_all(vap_handle* h, hipStream_t st) {
       if ((rc = cat(p + ".kvc", {p + ".mha_cross.key.weight", p + ".mha_cross.value.weight"}))) return rc;
       if ((rc = cat(p + ".oc", {p + ".mha_cross.proj.weight"}))) return rc;
       if ((rc = rp_copy(p + ".qc", D)) || (rc = rp_copy(p + ".kvc", 2 * D)) || (rc = rp_copy(p + ".oc", D))) return rc;
+      if constexpr (sizeof(T) == 2) {  // Q/K/V then cross K/V tiles back to back: the fused block's Wp
+        T* w = alloc(p + ".qkvkvc@rp", (int64_t)5 * D * D);
+        if (!w) return fail(VAP_ERR_HIP, "hipMalloc " + p + ".qkvkvc@rp");
+        HIPCHK(launch_pack_rowpanel((const bf16*)h->packed.at(p + ".qkv"), (bf16*)w, 3 * D, D, st));
+        HIPCHK(launch_pack_rowpanel((const bf16*)h->packed.at(p + ".kvc"), (bf16*)w + (int64_t)3 * D * D, 2 * D, D, st));
+      }
     }
     return VAP_OK;
   };
@@ -947,8 +957,11 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
 // bf16 transformer layer on frames [f0, f1) of EVERY sequence (time-chunked back end).  The layer's
 // Q/K/V (self) and K/V (cross) live in per-layer buffers so later chunks attend to earlier ones:
 // attention is causal, so queries [f0, f1) need keys [0, f1) only (modules.py:169-202).
+// With a next layer (`next` non-empty: its name, `ncross` whether it has cross attention) the block
+// kernel also writes that layer's Q/K/V and cross K/V rows; `projected`: this layer's were written so.
 int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, int li, int ci,
-                int f0, int f1, hipStream_t st, bf16* xb_out = nullptr) {
+                int f0, int f1, hipStream_t st, bf16* xb_out = nullptr, bool projected = false,
+                const std::string& next = "", bool ncross = false) {
   using T = bf16;
   const int T_ = p.T, S = p.S, nf = f1 - f0;
   const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
@@ -970,7 +983,7 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     a.gamma = h->P(ln + ".weight"); a.beta = h->P(ln + ".bias"); a.eps = 1e-5f; a.np = np; a.nr = nr;
     return launch_lnproj(a, st);
   };
-  {
+  if (!projected) {
     Timed tm(h, VAP_K_TR_GEMM, st);  // LN + QKV and the raw-row cross K/V from one read of x
     HIPCHK(lnp(nullptr, "", pre + ".qkv", 3, QKV + (int64_t)f0 * 3 * D, 3 * D, t3, pre + ".kvc", cross ? 2 : 0,
                KVC + (int64_t)f0 * 2 * D, 2 * D, t2, pre + ".ln_self_attn"));
@@ -1002,6 +1015,15 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
                 h->W<T>(pre + ".w1@rp"), h->W<T>(pre + ".w2@rp"), h->P(pre + ".ln_ffnetwork.weight"),
                 h->P(pre + ".ln_ffnetwork.bias"), 1e-5f};
     b.xb = xb_out ? xb_out + (int64_t)f0 * D : nullptr;
+    if (!next.empty()) {  // + the next layer's LN_self . QKV (and raw-row cross K/V) from the same rows
+      b.Wp = h->W<T>(next + (ncross ? ".qkvkvc@rp" : ".qkv@rp"));
+      b.cp = (T*)(ws + p.QKVL) + (int64_t)(li + 1) * S * t3 + (int64_t)f0 * 3 * D;
+      b.cr = ncross ? (T*)(ws + p.KVCL) + (int64_t)(cross ? ci + 1 : 0) * S * t2 + (int64_t)f0 * 2 * D : nullptr;
+      b.gamma2 = h->P(next + ".ln_self_attn.weight");
+      b.beta2 = h->P(next + ".ln_self_attn.bias");
+      b.np = 3;
+      b.nr = ncross ? 2 : 0;
+    }
     HIPCHK(launch_block(b, 0, st));
   }
   return VAP_OK;
@@ -1258,14 +1280,21 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
     const bool hchunk = h->heads_chunked && h->dims.cross_layers > 0;
-    int li = 0;
-    for (int l = 0; l < h->dims.channel_layers; ++l, ++li)
-      if ((rc = tr_layer_tc(h, p, ws, "ar_channel.layers." + std::to_string(l), false, li, 0, f0, f1, bst))) return rc;
-    for (int l = 0; l < h->dims.cross_layers; ++l, ++li) {
-      // the last layer's block kernel also writes x as bf16 (RAW): the combinator's input, so the
-      // heads need no separate fp32 -> bf16 pass over x
-      bf16* xb = l + 1 == h->dims.cross_layers ? (bf16*)(ws + p.RAW) : nullptr;
-      if ((rc = tr_layer_tc(h, p, ws, "ar.layers." + std::to_string(l), true, li, l, f0, f1, bst, xb))) return rc;
+    // layer list (name, cross attention, cross-K/V slot); the last layer's block kernel also writes x as
+    // bf16 (RAW): the combinator's input, so the heads need no separate fp32 -> bf16 pass over x
+    const int nl = h->dims.channel_layers + h->dims.cross_layers;
+    auto lname = [&](int i) {
+      return i < h->dims.channel_layers ? "ar_channel.layers." + std::to_string(i)
+                                        : "ar.layers." + std::to_string(i - h->dims.channel_layers);
+    };
+    for (int li = 0; li < nl; ++li) {
+      const bool cr = li >= h->dims.channel_layers, last = li + 1 == nl;
+      const int ci = cr ? li - h->dims.channel_layers : 0;
+      bf16* xb = cr && last ? (bf16*)(ws + p.RAW) : nullptr;
+      const bool fuse = h->block_fuse && !last;
+      if ((rc = tr_layer_tc(h, p, ws, lname(li), cr, li, ci, f0, f1, bst, xb, h->block_fuse && li > 0,
+                            fuse ? lname(li + 1) : std::string(), li + 1 >= h->dims.channel_layers)))
+        return rc;
     }
     if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bst))) return rc;
   }
@@ -1850,6 +1879,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
+  if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;

@@ -254,6 +254,16 @@ struct BlockArgs {
   const float* beta;
   float eps;
   bf16* xb = nullptr;  // optional bf16 copy of the output rows (same row layout as x)
+  // optional: the NEXT layer's LayerNorm'd projections from the same rows (np == 3), as lnproj's
+  // no-out-projection form: cp = LN2(x) . Wp[0:np)^T (the Q/K/V rows, np x 256 wide), cr = x . Wp[np:np+nr)^T
+  // (the raw-row cross K/V, nr x 256 wide); Wp holds the np + nr packed 256-wide tiles back to back; cp / cr
+  // rows sit where x's do with the row and sequence strides scaled by np / nr
+  const void* Wp = nullptr;
+  bf16* cp = nullptr;
+  bf16* cr = nullptr;
+  const float* gamma2 = nullptr;
+  const float* beta2 = nullptr;
+  int np = 0, nr = 0;
 };
 hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st);
 // combinator + vap_head in one launch (k_block.hip heads_kernel): logits [M][256] fp32 of frames
