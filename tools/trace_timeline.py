@@ -2,7 +2,10 @@
 """Timeline of the last forward in a rocprofv3 kernel trace: every kernel of the last LSTM launch's
 window, start / end relative to the LSTM start (us), grouped by kernel class.
 
-    python tools/trace_timeline.py gpurun_out/prof_x/run_kernel_trace.csv
+    python tools/trace_timeline.py gpurun_out/prof_x/run_kernel_trace.csv [pick]
+
+pick: which LSTM launch (python index, default -3: bench.py ends with a per-class timing pass and an
+isolated pass of the dominant class after the timed forwards)
 """
 import csv
 import sys
@@ -22,7 +25,8 @@ def main():
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Queue_Id"]) for r in rows]
     ks.sort()
     lstm = [k for k in ks if k[2] in ("lstm_resident", "lstm_pair")]
-    L = lstm[-2] if len(lstm) > 1 else lstm[-1]  # the last timed forward (the very last may be a breakdown pass)
+    pick = int(sys.argv[2]) if len(sys.argv) > 2 else -3
+    L = lstm[pick] if len(lstm) >= -pick else lstm[0]  # the last timed forward
     t0 = L[0]
     win = [k for k in ks if k[0] >= L[0] - 3_000_000 and k[0] <= L[1] + 3_000_000]
     prev_end = None

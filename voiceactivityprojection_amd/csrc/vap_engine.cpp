@@ -95,6 +95,7 @@ struct vap_handle {
   // cross K/V) from the rows it holds, one launch and one read of x less per layer transition
   // (VAP_BLOCK_FUSE=0: separate lnproj launches)
   bool block_fuse = true;
+  bool fe_join_late = true;  // VAP_FE_JOIN=0: the back end waits for the whole front-end stream
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
   // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
@@ -1245,8 +1246,11 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
 
 // Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
 // every transformer layer on the chunk's frames; then heads over all clips and the join.
+// fe_join (optional): the front-end stream's completion, joined into st at the end only (the back end
+// reads the recurrence's h rows, which the done[] hand-off orders; nothing the front end writes)
 int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& sy, unsigned char* ws, float* logits,
-                float* vadl, hipStream_t st, const unsigned* kernel_expect = nullptr, bool join = true) {
+                float* vadl, hipStream_t st, const unsigned* kernel_expect = nullptr, bool join = true,
+                hipEvent_t fe_join = nullptr) {
   using T = bf16;
   const int S = p.S, T_ = p.T;
   const int64_t t1 = (int64_t)T_ * D;
@@ -1300,6 +1304,7 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
   }
   if (!(h->heads_chunked && h->dims.cross_layers > 0) && (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst, true)))
     return rc;
+  if (fe_join) HIPCHK(hipStreamWaitEvent(st, fe_join, 0));
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
@@ -1448,12 +1453,19 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
       if (published != h->test_drop_ready)
         HIPCHK(hipStreamWriteValue32(fst && !ser ? fst : st, (void*)(sy.ready + published), sy.epoch, 0));
   }
-  if (fst) {  // join: the back end (and anything after the forward on st) follows the whole front end
-    hipEvent_t jn = h->next_fork_event();
+  // join: anything after the forward on st follows the whole front end.  The back end itself waits
+  // only for the recurrence (done[] flags), so its first chunk may start while the front-end stream
+  // still runs the last piece's conv2..4 and gate projections (VAP_FE_JOIN=0: join before it)
+  hipEvent_t jn = nullptr;
+  if (fst) {
+    jn = h->next_fork_event();
     HIPCHK(hipEventRecord(jn, fst));
-    HIPCHK(hipStreamWaitEvent(st, jn, 0));
+    if (!h->fe_join_late) {
+      HIPCHK(hipStreamWaitEvent(st, jn, 0));
+      jn = nullptr;
+    }
   }
-  return tc_back_end(h, p, t, sy, ws, logits, vadl, st);
+  return tc_back_end(h, p, t, sy, ws, logits, vadl, st, nullptr, true, jn);
 }
 
 // VapGPT.forward (model.py:249-268).  Micro-batch pipeline: the batch is split into up to
@@ -1880,6 +1892,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
+  if (const char* e = getenv("VAP_FE_JOIN")) h->fe_join_late = atoi(e) != 0;
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;
