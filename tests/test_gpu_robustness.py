@@ -200,3 +200,17 @@ def test_exchange_tags_across_launch_sizes_and_wrap():
     ref = fresh.probs(long)
     for k in ref:
         assert torch.equal(out[k], ref[k]), k
+
+
+def test_first_forward_equals_later():
+    """The first forward of a fresh model (cold caches, slow DMA) equals the later ones bit for bit.
+    It did not: the gate-projection GEMM's second ping-pong wave group waited for its own LDS-DMA of
+    stage k+1 one barrier after the first group began reading it, and a late piece was read stale
+    (k_gemm2.hip RAW note; 20 clips: 40 sequences, a partial recurrence group)."""
+    m = _model()
+    w = _batch(20, 320000, 300)
+    first = m.probs(w)
+    later = m.probs(w)
+    m.synchronize()
+    for k in first:
+        assert torch.equal(first[k], later[k]), k

@@ -139,8 +139,9 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   // a LOAD phase (issue the DMA three stages ahead, read this stage's fragments) and a COMPUTE phase
   // (32 MFMAs), each closed by a workgroup barrier; group 1 enters one barrier late, so on every
   // SIMD one wave's MFMAs overlap the other wave's LDS reads.
-  //   RAW: a wave waits (counted vmcnt) for its own DMA of stage t+1 at the end of COMPUTE t, before
-  //        the barrier that precedes any wave's first read of stage t+1.
+  //   RAW: a wave waits (counted vmcnt) for its own DMA of stage t+1 before the barrier that precedes
+  //        any wave's first read of stage t+1: group 0 at the end of COMPUTE t, group 1 (one barrier
+  //        behind) at the end of LOAD t, which meets group 0's end-of-COMPUTE barrier.
   //   WAR: stage t+3 overwrites stage t-1's buffer; its last reads (group 1's LOAD t-1) retire with
   //        lgkmcnt(0) before the barrier that precedes group 0's LOAD t.
   const int grp = wave >> 2;
@@ -172,6 +173,14 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
       af[i] = *(const chunk16*)(abase + row * ROWB + swz(row, fc) * 16);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // group 1's own DMA of stage kt+1 must land before THIS barrier: it is the one after which group 0
+    // reads stage kt+1 (group 1's own end-of-COMPUTE wait comes one barrier later; a late piece was
+    // read stale by a group-0 wave)
+    if (grp == 1) {
+      if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_sched_barrier(0);
     stamp(kt, 1);
     __builtin_amdgcn_s_barrier();

@@ -96,6 +96,7 @@ struct vap_handle {
   // (VAP_BLOCK_FUSE=0: separate lnproj launches)
   bool block_fuse = true;
   bool fe_join_late = true;  // VAP_FE_JOIN=0: the back end waits for the whole front-end stream
+  int be_split = 1;  // VAP_BE_SPLIT=2: the time-chunked back end in two sequence halves on two streams (tc_back_end)
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
   // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
@@ -135,6 +136,7 @@ struct vap_handle {
         hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && wv) {
       if (hipMalloc(&sync_mem, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
       if (hipMemset(sync_mem, 0, (2 * MAXMB + 1) * sizeof(unsigned)) != hipSuccess) return VAP_ERR_HIP;
+      if (hipDeviceSynchronize() != hipSuccess) return VAP_ERR_HIP;  // (null stream vs non-blocking side streams)
       if (hipHostMalloc((void**)&err_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
           hipHostGetDevicePointer((void**)&err_dev, err_host, 0) != hipSuccess)
         return VAP_ERR_HIP;
@@ -962,15 +964,17 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
 // kernel also writes that layer's Q/K/V and cross K/V rows; `projected`: this layer's were written so.
 int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::string& pre, bool cross, int li, int ci,
                 int f0, int f1, hipStream_t st, bf16* xb_out = nullptr, bool projected = false,
-                const std::string& next = "", bool ncross = false) {
+                const std::string& next = "", bool ncross = false, int s0 = 0, int sn = -1) {
+  // sequences [s0, s0 + sn) only (s0 even: cross attention pairs s with s ^ 1); layer strides stay p.S
   using T = bf16;
-  const int T_ = p.T, S = p.S, nf = f1 - f0;
+  const int T_ = p.T, S = sn < 0 ? p.S : sn, nf = f1 - f0;
   const int64_t t1 = (int64_t)T_ * D, t2 = 2 * t1, t3 = 3 * t1;
-  float* X = (float*)(ws + p.X);
-  T* QKV = (T*)(ws + p.QKVL) + (int64_t)li * S * t3;
-  T* KVC = (T*)(ws + p.KVCL) + (int64_t)ci * S * t2;
-  T* QC = (T*)(ws + p.QC);
-  T* ATT = (T*)(ws + p.ATT);
+  float* X = (float*)(ws + p.X) + (int64_t)s0 * t1;
+  T* QKV = (T*)(ws + p.QKVL) + (int64_t)li * p.S * t3 + (int64_t)s0 * t3;
+  T* KVC = (T*)(ws + p.KVCL) + (int64_t)ci * p.S * t2 + (int64_t)s0 * t2;
+  T* QC = (T*)(ws + p.QC) + (int64_t)s0 * t1;
+  T* ATT = (T*)(ws + p.ATT) + (int64_t)s0 * t1;
+  if (xb_out) xb_out += (int64_t)s0 * t1;
   const int H = h->dims.num_heads;
   const float scale = 1.0f / std::sqrt((float)D);
   float* Xf = X + (int64_t)f0 * D;
@@ -1018,8 +1022,9 @@ int tr_layer_tc(vap_handle* h, const Plan& p, unsigned char* ws, const std::stri
     b.xb = xb_out ? xb_out + (int64_t)f0 * D : nullptr;
     if (!next.empty()) {  // + the next layer's LN_self . QKV (and raw-row cross K/V) from the same rows
       b.Wp = h->W<T>(next + (ncross ? ".qkvkvc@rp" : ".qkv@rp"));
-      b.cp = (T*)(ws + p.QKVL) + (int64_t)(li + 1) * S * t3 + (int64_t)f0 * 3 * D;
-      b.cr = ncross ? (T*)(ws + p.KVCL) + (int64_t)(cross ? ci + 1 : 0) * S * t2 + (int64_t)f0 * 2 * D : nullptr;
+      b.cp = (T*)(ws + p.QKVL) + (int64_t)(li + 1) * p.S * t3 + (int64_t)s0 * t3 + (int64_t)f0 * 3 * D;
+      b.cr = ncross ? (T*)(ws + p.KVCL) + (int64_t)(cross ? ci + 1 : 0) * p.S * t2 + (int64_t)s0 * t2 + (int64_t)f0 * 2 * D
+                    : nullptr;
       b.gamma2 = h->P(next + ".ln_self_attn.weight");
       b.beta2 = h->P(next + ".ln_self_attn.bias");
       b.np = 3;
@@ -1075,12 +1080,15 @@ int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer
     const size_t bytes = std::max(need, (size_t)64 * slot);
     HIPCHK(hipMalloc(&h->xbuf, bytes));
     HIPCHK(hipMemset(h->xbuf, 0, bytes));  // tags are >= 1: zero never matches
+    // (hipMemset runs on the null stream, which the non-blocking side streams do not wait for)
+    HIPCHK(hipDeviceSynchronize());
     h->xbuf_bytes = bytes;
   }
   const uint64_t span = (uint64_t)L4 + 1;
   if ((uint64_t)h->xtag + span + 1 > 0xFFFFFFFFull) {  // tag space exhausted (~4e9 steps): restart at 1
     HIPCHK(hipDeviceSynchronize());                    // no launch may still read the old tags
     HIPCHK(hipMemset(h->xbuf, 0, h->xbuf_bytes));
+    HIPCHK(hipDeviceSynchronize());  // cleared before the launch on a non-blocking side stream reads it
     h->xtag = 0;
   }
   const unsigned tag0 = h->xtag + 1;  // this launch: tags tag0 .. tag0 + L4
@@ -1226,12 +1234,15 @@ int tc_launch_lstm(vap_handle* h, const Plan& p, const TcSched& t, const bf16* G
 // only the last chunk's remain after the recurrence.  RAW holds the bf16 copy of the final x that
 // the last layer's block kernel wrote.
 int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, float* logits, float* vadl,
-             hipStream_t st) {
+             hipStream_t st, int c0 = 0, int nb = -1) {
+  // clips [c0, c0 + nb) only (sequences 2 c0 ..)
   using T = bf16;
-  const int T_ = p.T, nf = f1 - f0, B = p.B;
+  const int T_ = p.T, nf = f1 - f0, B = nb < 0 ? p.B : nb;
   const int64_t t1 = (int64_t)T_ * D;
-  float* X = (float*)(ws + p.X);
-  T* RAW = (T*)(ws + p.RAW);
+  float* X = (float*)(ws + p.X) + (int64_t)2 * c0 * t1;
+  T* RAW = (T*)(ws + p.RAW) + (int64_t)2 * c0 * t1;
+  logits += (int64_t)c0 * T_ * 256;
+  vadl += (int64_t)c0 * T_ * 2;
   Timed tm(h, VAP_K_HEADS, st);
   const int64_t o = (int64_t)f0 * D;
   // heads_kernel on the frame range [f0, f0 + nf) of every clip
@@ -1242,6 +1253,17 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
   ha.xf = X + o;
   HIPCHK(launch_heads(ha, st));
   return VAP_OK;
+}
+
+// Sequence groups of the time-chunked back end (1 or 2, see tc_back_end).  Two need: the front end on
+// side[1] (its join event passed in), per-chunk heads, whole clips in each half, and no back-end class
+// timed (vap_timing brackets one stream's launches).
+static int be_split_ways(const vap_handle* h, const Plan& p, bool fe_on_side1) {
+  if (h->be_split < 2 || !fe_on_side1 || h->fe_stream || !h->heads_chunked || h->dims.cross_layers <= 0 || p.B < 2)
+    return 1;
+  const int tc = h->timing_cls;
+  if (tc == VAP_K_DOWNSAMPLE || tc == VAP_K_TR_GEMM || tc == VAP_K_ATTN || tc == VAP_K_HEADS) return 1;
+  return 2;
 }
 
 // Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
@@ -1264,23 +1286,30 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     HIPCHK(hipEventRecord(fk, st));
     HIPCHK(hipStreamWaitEvent(bst, fk, 0));
   }
+  // be_split = 2 (sequence halves on two streams: the caller's and the front-end stream, which joins
+  // once the last front-end piece is done): each launch's last partial round of workgroups, and the
+  // attention (VALU / MFMA) beside the row kernels (HBM), share the chip with the other half's launches
+  const int nsp = be_split_ways(h, p, fe_join != nullptr && !kernel_expect && bst == st);
   int rc;
   for (int k = 0; k < t.nbe; ++k) {
     const int c = t.be_end[k] - 1;  // the last recurrence chunk of back-end chunk k
     const int f0 = t.fb[k ? t.be_end[k - 1] : 0], f1 = t.fb[c + 1];
+   for (int g = 0; g < nsp; ++g) {
+    const int sq0 = nsp == 1 ? 0 : (p.B * g / nsp) * 2, sq1 = nsp == 1 ? S : (p.B * (g + 1) / nsp) * 2;
+    const hipStream_t bs = g == 0 ? bst : h->side[1];
     if (kernel_expect)  // captured streaming push: the hand-off as a kernel (graph-capturable)
-      HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bst));
+      HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bs));
     else
-      HIPCHK(hipStreamWaitValue32(bst, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
+      HIPCHK(hipStreamWaitValue32(bs, sy.done + c, h->done_expect[c], hipStreamWaitValueGte, 0xFFFFFFFFu));
     {  // downsample: CConv1d k5 s2 causal + LayerNorm + GELU (encoder_components.py:485-499)
-      Timed tm(h, VAP_K_DOWNSAMPLE, bst);
-      GemmArgs ga = gargs(Hf + (int64_t)f0 * 2 * D, 2 * D, p.sh, h->W<T>("down"), 5 * D, D,
-                          h->P("encoder.downsample.1.bias"), f1 - f0, S, X + (int64_t)f0 * D, D, t1);
+      Timed tm(h, VAP_K_DOWNSAMPLE, bs);
+      GemmArgs ga = gargs(Hf + (int64_t)sq0 * p.sh + (int64_t)f0 * 2 * D, 2 * D, p.sh, h->W<T>("down"), 5 * D, D,
+                          h->P("encoder.downsample.1.bias"), f1 - f0, sq1 - sq0, X + (int64_t)sq0 * t1 + (int64_t)f0 * D, D, t1);
       ga.norm = 2;
       ga.act = 2;
       ga.gamma = h->P("encoder.downsample.2.ln.weight");
       ga.beta = h->P("encoder.downsample.2.ln.bias");
-      HIPCHK(gemm<T>(ga, bst, true));
+      HIPCHK(gemm<T>(ga, bs, true));
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
     const bool hchunk = h->heads_chunked && h->dims.cross_layers > 0;
@@ -1296,14 +1325,19 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       const int ci = cr ? li - h->dims.channel_layers : 0;
       bf16* xb = cr && last ? (bf16*)(ws + p.RAW) : nullptr;
       const bool fuse = h->block_fuse && !last;
-      if ((rc = tr_layer_tc(h, p, ws, lname(li), cr, li, ci, f0, f1, bst, xb, h->block_fuse && li > 0,
-                            fuse ? lname(li + 1) : std::string(), li + 1 >= h->dims.channel_layers)))
+      if ((rc = tr_layer_tc(h, p, ws, lname(li), cr, li, ci, f0, f1, bs, xb, h->block_fuse && li > 0,
+                            fuse ? lname(li + 1) : std::string(), li + 1 >= h->dims.channel_layers, sq0, sq1 - sq0)))
         return rc;
     }
-    if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bst))) return rc;
+    if (hchunk && (rc = heads_tc(h, p, ws, f0, f1, logits, vadl, bs, sq0 / 2, (sq1 - sq0) / 2))) return rc;
+   }
   }
   if (!(h->heads_chunked && h->dims.cross_layers > 0) && (rc = heads<T>(h, p, ws, Range{0, p.B}, logits, vadl, bst, true)))
     return rc;
+  if (nsp > 1) {  // the second half ran on the front-end stream, after its last piece: that joins both
+    fe_join = h->next_fork_event();
+    HIPCHK(hipEventRecord(fe_join, h->side[1]));
+  }
   if (fe_join) HIPCHK(hipStreamWaitEvent(st, fe_join, 0));
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
@@ -1893,6 +1927,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
   if (const char* e = getenv("VAP_FE_JOIN")) h->fe_join_late = atoi(e) != 0;
+  if (const char* e = getenv("VAP_BE_SPLIT")) h->be_split = atoi(e);
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;
