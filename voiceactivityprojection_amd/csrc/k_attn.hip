@@ -201,7 +201,11 @@ VAP_DEV u32x2 tr_read(const unsigned char* p) {
 // q-block (FETCH_SIZE 319 -> 96 MB per 128-sequence launch; a longest-first order over all pairs
 // puts one pair's q-blocks far apart in time).
 // Measured and dropped: K / V tiles by LDS-DMA into a 3-slot ring two tiles ahead with the K
-// fragments of a 32-key half read together (no faster: 149 vs 149 us per 128 x 1000 launch).
+// fragments of a 32-key half read together (no faster: 149 vs 149 us per 128 x 1000 launch); a
+// software pipeline across key tiles (S_j issued, then the previous tile's P.V, then tile j's softmax
+// beside those MFMAs; V one tile behind K in LDS): 194 VGPRs, 2 waves per SIMD, 0.92 -> 1.03-1.09 ms
+// per bench step (forced to 3 waves: 13 spilled VGPRs, 1.34 ms) -- the third wave per SIMD already
+// hides the softmax behind another wave's MFMAs better than one wave's own pipeline.
 // ------------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VAP_DEV f32x16 mfma32(chunk16 a, chunk16 b, f32x16 c) {
@@ -386,197 +390,6 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// attn5: attn4 software-pipelined across key tiles.  Iteration j issues S_j = K_j Q'^T, then the
-// previous tile's O += V_{j-1}^T P_{j-1} (and its row sums), then runs tile j's softmax VALU while
-// the matrix pipe still works through the P.V MFMAs, so one wave's exp2 / max / convert stream
-// overlaps its own MFMAs instead of waiting on them (attn4 ran them back to back per tile and
-// relied on 3 waves per SIMD to fill the gaps).  V lags K by one tile in LDS: iteration j writes
-// K_{j+1} into K slot (j+1)&1 and V_j into V slot j&1, both last read in iteration j-1, so one
-// barrier per tile still orders every slot.  A rescale of O (lazy, as attn4) applies after the
-// pending P_{j-1}.V_{j-1} landed in O (data dependence), which was relative to the old max: exact.
-// ------------------------------------------------------------------------------------------
-#ifndef ATTN5_OCC
-#define ATTN5_OCC 2
-#endif
-__global__ __launch_bounds__(256, ATTN5_OCC) void attn5_kernel(AttnArgs a, int nqb, int grp) {
-  __shared__ __attribute__((aligned(16))) unsigned char ksm[2][KB2 * TROW];
-  __shared__ __attribute__((aligned(16))) unsigned char vsm[2][KB2 * TROW];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int npair = a.H * a.S;
-  int hs, qb;
-  if (grp > 0 && (npair & 7) == 0) {
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, px = npair >> 3;
-    const int g = j / (grp * nqb), r = j - g * grp * nqb;
-    const int gp = min(grp, px - g * grp);
-    const int lv = r / gp;
-    qb = nqb - 1 - lv;
-    hs = (g * grp + (r - lv * gp)) * 8 + x;
-  } else {
-    hs = blockIdx.x % npair;
-    qb = nqb - 1 - (int)(blockIdx.x / npair);
-  }
-  const int h = hs % a.H, s = hs / a.H;
-  const int ks = a.kv_swap ? (s ^ 1) : s;
-  const bf16* Qs = (const bf16*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
-  const __amdgpu_buffer_rsrc_t rK = make_rsrc((const bf16*)a.K + (int64_t)ks * a.k_seq + h * HDIM, (uint32_t)a.T * a.k_ld * 2);
-  const __amdgpu_buffer_rsrc_t rV = make_rsrc((const bf16*)a.V + (int64_t)ks * a.v_seq + h * HDIM, (uint32_t)a.T * a.v_ld * 2);
-  constexpr float LOG2E = 1.4426950408889634f;
-  constexpr float TAU = 8.0f;
-  const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
-  const int qw0 = a.q0 + qb * QB2 + w * 32;
-  const int qlast = min(a.q0 + qb * QB2 + QB2 - 1, a.T - 1);
-  const int nkb = qlast / KB2 + 1;
-  const int nvis = min(nkb, (qw0 + 31) / KB2 + 1);  // tiles with a key visible to some query of the wave
-  const int hl = lane >> 5, ql = lane & 31;
-  const int qv = qw0 + ql;
-
-  chunk16 qf[4];
-  {
-    const int qc = qv < a.T ? qv : a.T - 1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bf16x8 q = *(const bf16x8*)(Qs + (int64_t)qc * a.q_ld + 16 * k + 8 * hl);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = (bf16)((float)q[e] * c2);
-      qf[k] = __builtin_bit_cast(chunk16, q);
-    }
-  }
-  f32x16 kb0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) kb0[r] = sl2 * (float)(8 * (r >> 2) + 4 * hl + (r & 3));
-  const float off32 = sl2 * 32.0f, off64 = sl2 * (float)KB2;
-
-  float m = -INFINITY;
-  f32x16 o0 = {}, o1 = {}, ls = {};
-  const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
-  const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
-
-  const int srow = tid >> 3, sc = tid & 7;
-  const uint32_t vkoff0 = (uint32_t)(srow * a.k_ld + sc * 8) * 2, vkoff1 = vkoff0 + 32u * a.k_ld * 2;
-  const uint32_t vvoff0 = (uint32_t)(srow * a.v_ld + sc * 8) * 2, vvoff1 = vvoff0 + 32u * a.v_ld * 2;
-  const uint32_t ktile = (uint32_t)KB2 * a.k_ld * 2, vtile = (uint32_t)KB2 * a.v_ld * 2;
-  const int ldsK0 = srow * TROW + kswz2(srow, sc) * 16, ldsK1 = (srow + 32) * TROW + kswz2(srow + 32, sc) * 16;
-  const int ldsV0 = srow * TROW + vswz4(srow, sc) * 16, ldsV1 = (srow + 32) * TROW + vswz4(srow + 32, sc) * 16;
-  chunk16 rk[2], rv[2];
-  int koff[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) koff[k] = ql * TROW + kswz2(ql, 2 * k + hl) * 16;
-  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
-  int voff[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    voff[u] = (4 * hl + tq) * TROW + vswz4(4 * hl + tq, 4 * u + 2 * tg + (tp >> 1)) * 16 + (tp & 1) * 8;
-
-  bf16x8 pb[2][2];  // P of the pending tile (bf16, the B operand of its P.V MFMAs)
-  // O^T += V^T P^T of tile `t` (V slot vs)
-  auto pv = [&](int vs) {
-    const unsigned char* Vt = vsm[vs];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const chunk16 p = __builtin_bit_cast(chunk16, pb[t][k]);
-        const int ro = (32 * t + 16 * k) * TROW;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const u32x2 v0 = tr_read(Vt + ro + voff[u]);
-          const u32x2 v1 = tr_read(Vt + ro + 8 * TROW + voff[u]);
-          const chunk16 vf = {v0.x, v0.y, v1.x, v1.y};
-          if (u == 0) o0 = mfma32(vf, p, o0);
-          else o1 = mfma32(vf, p, o1);
-        }
-        ls = mfma32(ones, p, ls);
-      }
-  };
-
-  // prologue: K_0 into K slot 0
-  rk[0] = buf_load16(rK, vkoff0, 0);
-  rk[1] = buf_load16(rK, vkoff1, 0);
-  *(chunk16*)(ksm[0] + ldsK0) = rk[0];
-  *(chunk16*)(ksm[0] + ldsK1) = rk[1];
-  __syncthreads();
-
-  auto iter = [&](int kb, auto par_c) {
-    constexpr int par = decltype(par_c)::value;  // kb & 1
-    if (kb + 1 < nkb) {
-      rk[0] = buf_load16(rK, vkoff0, (kb + 1) * ktile);
-      rk[1] = buf_load16(rK, vkoff1, (kb + 1) * ktile);
-    }
-    rv[0] = buf_load16(rV, vvoff0, kb * vtile);
-    rv[1] = buf_load16(rV, vvoff1, kb * vtile);
-    if (kb < nvis) {  // wave-uniform
-      const int key0 = kb * KB2;
-      const unsigned char* Kt = ksm[par];
-      f32x16 st[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        st[t] = kb0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st[t] = mfma32(*(const chunk16*)(Kt + t * 32 * TROW + koff[k]), qf[k], st[t]);
-      }
-      if (kb > 0) pv(par ^ 1);  // the previous tile's P.V (visible: tiles are visible as a prefix)
-      if (key0 + KB2 - 1 > qw0) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (key0 + 32 * t + 8 * (r >> 2) + 4 * hl + (r & 3) > qv) st[t][r] = -INFINITY;
-      }
-      float b0 = st[0][0], b1 = st[1][0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) {
-        b0 = fmaxf(b0, st[0][r]);
-        b1 = fmaxf(b1, st[1][r]);
-      }
-      const float tofs = off64 * (float)kb;
-      const float bm = xmax2(fmaxf(b0, b1 + off32)) + tofs;
-      if (__ballot(bm > m + TAU)) {
-        const float mn = fmaxf(m, bm);
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        m = mn;
-        o0 *= alpha;
-        o1 *= alpha;
-        ls *= alpha;
-      }
-      const float m0 = m - tofs, m1 = m0 - off32;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const float mt = t ? m1 : m0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) pb[t][k][e] = (bf16)__builtin_amdgcn_exp2f(st[t][8 * k + e] - mt);
-        }
-    } else if (kb == nvis) {
-      pv(par ^ 1);  // the wave's last visible tile
-    }
-    if (kb + 1 < nkb) {
-      *(chunk16*)(ksm[par ^ 1] + ldsK0) = rk[0];
-      *(chunk16*)(ksm[par ^ 1] + ldsK1) = rk[1];
-    }
-    *(chunk16*)(vsm[par] + ldsV0) = rv[0];
-    *(chunk16*)(vsm[par] + ldsV1) = rv[1];
-    __syncthreads();
-  };
-  for (int kb = 0; kb < nkb; kb += 2) {
-    iter(kb, std::integral_constant<int, 0>{});
-    if (kb + 1 < nkb) iter(kb + 1, std::integral_constant<int, 1>{});
-  }
-  if (nvis == nkb) pv((nkb - 1) & 1);  // the last tile's P.V (V_{nkb-1} written and published above)
-
-  const float inv = 1.0f / ls[0];
-  if (qv < a.T) {
-    bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv * a.o_ld + h * HDIM;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      store4(orow + 8 * g + 4 * hl, o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-      store4(orow + 32 + 8 * g + 4 * hl, o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-    }
-  }
-}
-
-
 }  // namespace
 
 template <typename T>
@@ -586,11 +399,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
     if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
     const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
     constexpr int grp = 8;  // (sequence, head) pairs per XCD group: K/V of 8 pairs x <= 256 KiB in L2
-#if VAP_ATTN_PIPE
-    hipLaunchKernelGGL(attn5_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
-#else
     hipLaunchKernelGGL(attn4_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
-#endif
     return hipGetLastError();
   }
   if (a.q0 != 0) return hipErrorInvalidValue;

@@ -36,8 +36,8 @@ constexpr int ROWB = D * 2;  // bf16 row of the panel / of a hidden slice: 512 B
 // cycles per SIMD, so 2 in flight leave the L2 round trip exposed; 8 in flight cost 48 VGPRs,
 // which drops the 64-row kernels from two workgroups per CU to one
 
-template <int MT, int RH = 1> struct Blk {  // RH row halves of 16 MT rows (RH = 2: 16 waves, 1024 threads)
-  static constexpr int R = 16 * MT * RH;
+template <int MT> struct Blk {
+  static constexpr int R = 16 * MT;
   static constexpr int OFF_H = R * ROWB;
   static constexpr int OFF_RED = 2 * R * ROWB;  // [2][R][8] fp32 per-wave row partials
   static constexpr int OFF_GB = OFF_RED + 2 * R * 8 * 4;  // LayerNorm gamma / beta
@@ -146,27 +146,22 @@ VAP_DEV void ln_panel(const f32x4 (&acc)[2][MT], float* red0, float* red1, const
 // issued, [17] stores complete
 __device__ unsigned long long g_blk_stamps[8][24];
 
-template <int MT, bool OPROJ, bool ST = false, int NPF = 2, int NP2 = 0, int NR2 = 0, int RH = 1>
-__global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
-  // RH = 2: two 64-row halves in one workgroup of 16 waves (waves w and w + 8 own the same columns of
-  // the two halves): both halves read every weight fragment at about the same time, so the second
-  // read hits the CU's L1 and the L2 streams the weights once per 128 rows instead of once per 64
-  using C = Blk<MT, RH>;
-  constexpr int R = 16 * MT;  // rows of this wave's half
+template <int MT, bool OPROJ, bool ST = false, int NPF = 2, int NP2 = 0, int NR2 = 0>
+__global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
+  using C = Blk<MT>;
+  constexpr int R = C::R;
   constexpr int Q0 = OPROJ ? 8 : 0;      // first FFN k-step of the weight stream
   constexpr int Q2 = Q0 + 48;            // first k-step of the fused next-layer projections
   constexpr int NQ = Q2 + 8 * (NP2 + NR2);  // Wo 8 + 3 x (W1 8 + W2 8) [+ Wp / Wr 8 per N tile]
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
-  const int tid0 = threadIdx.x, lane = tid0 & 63, l16 = lane & 15, lg = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-  const int whalf = RH > 1 ? wv >> 3 : 0, w = RH > 1 ? wv & 7 : wv;  // row half, column group
-  const int tid = RH > 1 ? tid0 & 511 : tid0;                       // thread within the half
-  unsigned char* P = smem + whalf * R * ROWB;
-  unsigned char* H = smem + C::OFF_H + whalf * R * ROWB;
-  float* red0 = (float*)(smem + C::OFF_RED) + whalf * R * 8;
-  float* red1 = (float*)(smem + C::OFF_RED) + C::R * 8 + whalf * R * 8;
-  const int m0 = (blockIdx.x * RH + whalf) * R;
-  const int samp = (ST && (blockIdx.x & 31) == 0 && blockIdx.x < 256 && tid0 == 0) ? (int)(blockIdx.x >> 5) : -1;
+  unsigned char* P = smem;
+  unsigned char* H = smem + C::OFF_H;
+  float* red0 = (float*)(smem + C::OFF_RED);
+  float* red1 = red0 + R * 8;
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * R;
+  const int samp = (ST && (blockIdx.x & 31) == 0 && blockIdx.x < 256 && tid == 0) ? (int)(blockIdx.x >> 5) : -1;
   // phase boundary (+ a stamp in the diagnostics build): the scheduling barrier also keeps the
   // scheduler from mixing phases, which otherwise drives the 144-row variant into spills
   unsigned long long stv[18];  // wave-uniform: SGPRs
@@ -192,7 +187,7 @@ __global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
   // gamma / beta of the LayerNorm -> LDS (issued first: vmcnt counts in order)
   float* GB = (float*)(smem + C::OFF_GB);
   f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
-  if (tid0 < 128) gbv = *(const f32x4*)((tid0 < 64 ? g.gamma : g.beta) + (tid0 & 63) * 4);
+  if (tid < 128) gbv = *(const f32x4*)((tid < 64 ? g.gamma : g.beta) + (tid & 63) * 4);
 
   // ---------------------------------------------------------------- O panel (bf16) and residual rows
   // O first, so the out-projection waits for O only while x is still in flight; rows >= M read 0
@@ -284,7 +279,7 @@ __global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
       const int id = tid + k * 512, row = id >> 5, c = id & 31;
       *(chunk16*)(H + row * ROWB + xswz(row, c) * 16) = ot[k];
     }
-    if (tid0 < 128) *(f32x4*)(GB + tid0 * 4) = gbv;
+    if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
     __syncthreads();
     stamp(1);
 #pragma unroll
@@ -295,7 +290,7 @@ __global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
       for (int j = 0; j < MT; ++j) acc[i][j] += xt[i][j];
     stamp(2);
   } else {
-    if (tid0 < 128) *(f32x4*)(GB + tid0 * 4) = gbv;
+    if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
   }
 
   // ---------------------------------------------------------------- LayerNorm(x') -> P
@@ -367,7 +362,7 @@ __global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
     // through the FFN (+20 VGPRs, half the occupancy)
     int z2;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z2));
-    const int tidb = tid0 + z2, l16b = l16 + z2, lgb = lg + z2;
+    const int tidb = tid + z2, l16b = l16 + z2, lgb = lg + z2;
     // this phase's arguments read here from the kernel-argument segment through an opaque pointer: held
     // from the prologue they spill SGPRs into a VGPR
     using KA = const __attribute__((address_space(4))) BlockArgs*;
@@ -443,16 +438,6 @@ __global__ __launch_bounds__(512 * RH, 1) void block_kernel(BlockArgs g) {
 
 template <int MT>
 hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
-#if VAP_BLOCK_RH2
-  if constexpr (MT == 4) {  // 128-row workgroups of 16 waves (two 64-row halves sharing the weight stream)
-    const dim3 grid2((g.M + 127) / 128);
-    if (g.np && g.nr) hipLaunchKernelGGL((block_kernel<4, true, false, 2, 3, 2, 2>), grid2, dim3(1024), 0, st, g);
-    else if (g.np) hipLaunchKernelGGL((block_kernel<4, true, false, 2, 3, 0, 2>), grid2, dim3(1024), 0, st, g);
-    else if (g.o) hipLaunchKernelGGL((block_kernel<4, true, false, 2, 0, 0, 2>), grid2, dim3(1024), 0, st, g);
-    else hipLaunchKernelGGL((block_kernel<4, false, false, 2, 0, 0, 2>), grid2, dim3(1024), 0, st, g);
-    return hipGetLastError();
-  }
-#endif
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
   static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
   static const int npf = getenv("VAP_BLOCK_NPF") ? atoi(getenv("VAP_BLOCK_NPF")) : 2;
@@ -522,26 +507,24 @@ namespace {
 // [10 + p] pass p's stores issued, [16] all stores complete
 __device__ unsigned long long g_lnp_stamps[8][24];
 
-template <int MT, bool OPROJ, int NP, int NR, bool ST = false, int NPF = 2, int RH = 1>
-__global__ __launch_bounds__(512 * RH, 1) void lnproj_kernel(LnProjArgs g) {
+template <int MT, bool OPROJ, int NP, int NR, bool ST = false, int NPF = 2>
+__global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
   static_assert(!(OPROJ && NR), "the raw panel shares H with the O panel");
-  using C = Blk<MT, RH>;  // RH = 2: two 64-row halves share the weight stream (see block_kernel)
-  constexpr int R = 16 * MT;
+  using C = Blk<MT>;
+  constexpr int R = C::R;
   constexpr int Q0 = OPROJ ? 8 : 0;
   constexpr int NQ = Q0 + 8 * (NP + NR);
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
-  const int tid0 = threadIdx.x, lane = tid0 & 63, l16 = lane & 15, lg = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-  const int whalf = RH > 1 ? wv >> 3 : 0, w = RH > 1 ? wv & 7 : wv;  // row half, column group
-  const int tid = RH > 1 ? tid0 & 511 : tid0;                          // thread within the half
-  unsigned char* P = smem + whalf * R * ROWB;
-  unsigned char* H = smem + C::OFF_H + whalf * R * ROWB;
-  float* red0 = (float*)(smem + C::OFF_RED) + whalf * R * 8;
-  float* red1 = (float*)(smem + C::OFF_RED) + C::R * 8 + whalf * R * 8;
+  unsigned char* P = smem;
+  unsigned char* H = smem + C::OFF_H;
+  float* red0 = (float*)(smem + C::OFF_RED);
+  float* red1 = red0 + R * 8;
   float* GB = (float*)(smem + C::OFF_GB);
-  const int m0 = (blockIdx.x * RH + whalf) * R;
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * R;
   const int rps = g.rows_per_seq;
-  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && tid0 == 0) ? (int)(blockIdx.x >> 6) : -1;
+  const int samp = (ST && (blockIdx.x & 63) == 0 && blockIdx.x < 512 && tid == 0) ? (int)(blockIdx.x >> 6) : -1;
   unsigned long long stv[17] = {};  // wave-uniform: SGPRs
   auto stamp = [&](int k) {
     if constexpr (ST) {
@@ -558,7 +541,7 @@ __global__ __launch_bounds__(512 * RH, 1) void lnproj_kernel(LnProjArgs g) {
   };
 
   f32x4 gbv = {0.f, 0.f, 0.f, 0.f};
-  if (tid0 < 128) gbv = *(const f32x4*)((tid0 < 64 ? g.gamma : g.beta) + (tid0 & 63) * 4);
+  if (tid < 128) gbv = *(const f32x4*)((tid < 64 ? g.gamma : g.beta) + (tid & 63) * 4);
 
   constexpr int OPT = R * 32 / 512;
   chunk16 ot[OPROJ ? OPT : 1];
@@ -619,7 +602,7 @@ __global__ __launch_bounds__(512 * RH, 1) void lnproj_kernel(LnProjArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  if (tid0 < 128) *(f32x4*)(GB + tid0 * 4) = gbv;
+  if (tid < 128) *(f32x4*)(GB + tid * 4) = gbv;
   if constexpr (OPROJ) {
 #pragma unroll
     for (int k = 0; k < OPT; ++k) {
@@ -701,16 +684,6 @@ __global__ __launch_bounds__(512 * RH, 1) void lnproj_kernel(LnProjArgs g) {
 
 template <int MT>
 hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
-#if VAP_BLOCK_RH2
-  if constexpr (MT == 4) {  // 128-row workgroups of 16 waves (two 64-row halves sharing the weight stream)
-    const dim3 grid2((g.M + 127) / 128);
-    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<4, true, 1, 0, false, 2, 2>), grid2, dim3(1024), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<4, false, 3, 0, false, 2, 2>), grid2, dim3(1024), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<4, false, 3, 2, false, 2, 2>), grid2, dim3(1024), 0, st, g);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-#endif
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
   static const bool stamps = getenv("VAP_LNPROJ_STAMPS") != nullptr;
   if (stamps) {

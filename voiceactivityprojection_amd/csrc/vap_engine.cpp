@@ -96,7 +96,7 @@ struct vap_handle {
   // (VAP_BLOCK_FUSE=0: separate lnproj launches)
   bool block_fuse = true;
   bool fe_join_late = true;  // VAP_FE_JOIN=0: the back end waits for the whole front-end stream
-  int be_split = 1;  // VAP_BE_SPLIT=2: the time-chunked back end in two sequence halves on two streams (tc_back_end)
+  int be_split = 2;  // VAP_BE_SPLIT=1: the time-chunked back end on the caller stream only (tc_back_end)
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
   // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
