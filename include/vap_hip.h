@@ -16,8 +16,11 @@
  * Conventions: plain pointers and sizes only.  Every tensor argument is a caller-allocated DEVICE
  * buffer (float32 unless stated, C-contiguous).  `stream` is a hipStream_t passed as void*.
  * All calls are asynchronous on `stream` except vap_timing_read.  Return value: VAP_OK or an
- * error code; vap_last_error() gives a message (thread-local).  No global mutable state: one
- * handle per model, reentrant across handles.
+ * error code; vap_last_error() gives a message (thread-local).  One handle per model, reentrant
+ * across handles.  The forward schedule is fixed at vap_create: the handle reads its developer
+ * overrides (VAP_TC_FE / VAP_TC_BE / VAP_BE_SPLIT / VAP_FE_STREAMS / ...) from the
+ * environment once, there; the defaults are the product.  Diagnostics builds aside (in-kernel
+ * stamps, read once per process), no launch depends on process state after that.
  */
 #ifndef VAP_HIP_H
 #define VAP_HIP_H

@@ -440,7 +440,6 @@ template <int MT>
 hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
   const dim3 grid((g.M + 16 * MT - 1) / (16 * MT));
   static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
-  static const int npf = getenv("VAP_BLOCK_NPF") ? atoi(getenv("VAP_BLOCK_NPF")) : 2;
   if (g.np) {  // fused next-layer projections (the 64-row variant only: launch_block forces MT 4)
     if constexpr (MT == 4) {
       if (g.nr) hipLaunchKernelGGL((block_kernel<MT, true, false, 2, 3, 2>), grid, dim3(512), 0, st, g);
@@ -449,9 +448,7 @@ hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
     }
     return hipErrorInvalidValue;
   }
-  if (stamps && g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, true, 8>), grid, dim3(512), 0, st, g);
-  else if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
-  else if (g.o && npf == 8) hipLaunchKernelGGL((block_kernel<MT, true, false, 8>), grid, dim3(512), 0, st, g);
+  if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
   else if (g.o) hipLaunchKernelGGL((block_kernel<MT, true>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((block_kernel<MT, false>), grid, dim3(512), 0, st, g);
   return hipGetLastError();
@@ -460,7 +457,7 @@ hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
 }  // namespace
 
 // rows per workgroup: 64 (MT 4: 70 KiB LDS and 126 VGPRs, so two workgroups share a CU and one's
-// HBM phases overlap the other's matrix work: 40 us per 32k rows) unless VAP_BLOCK_MT=9 (144 rows,
+// HBM phases overlap the other's matrix work: 40 us per 32k rows) unless a small `cus` asks for 144 rows (MT 9:
 // one workgroup per CU, weights streamed once per 144 rows: 47 us, its HBM load / store phases
 // exposed); `cus` = 0 selects the default, a positive count lets MT 9 take inputs that 2 x cus
 // 64-row workgroups would not cover in one round
@@ -469,8 +466,7 @@ hipError_t launch_block(const BlockArgs& g, int cus, hipStream_t st) {
   if (g.np && (g.np != 3 || (g.nr != 0 && g.nr != 2) || !g.o || !g.Wp || !g.cp || !g.gamma2 || !g.beta2 ||
                (g.nr && !g.cr)))
     return hipErrorInvalidValue;
-  static const int force = getenv("VAP_BLOCK_MT") ? atoi(getenv("VAP_BLOCK_MT")) : 0;
-  const int mt = g.np ? 4 : force ? force : (cus > 0 && cus < 64 && (g.M + 63) / 64 > 2 * cus ? 9 : 4);
+  const int mt = g.np ? 4 : (cus > 0 && cus < 64 && (g.M + 63) / 64 > 2 * cus ? 9 : 4);
   const int bm = 16 * mt;
   // a panel's rows must lie within the 2 GiB a buffer offset reaches from its first row
   const int64_t span = g.rows_per_seq ? (bm / g.rows_per_seq + 2) * g.x_seq + (int64_t)bm * D : (int64_t)bm * D;
@@ -690,21 +686,6 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
     if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, true>), grid, dim3(512), 0, st, g);
     else if (!g.o && g.np == 3 && g.nr == 2)
       hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, true>), grid, dim3(512), 0, st, g);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-  static const int npf = getenv("VAP_LNPROJ_NPF") ? atoi(getenv("VAP_LNPROJ_NPF")) : 2;
-  if (npf == 4) {  // 4 k-steps in flight still fits two workgroups per CU (<= 128 VGPRs)
-    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, 4>), grid, dim3(512), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, 4>), grid, dim3(512), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, false, 4>), grid, dim3(512), 0, st, g);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
-  if (npf == 8) {
-    if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, 8>), grid, dim3(512), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, 8>), grid, dim3(512), 0, st, g);
-    else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, false, 8>), grid, dim3(512), 0, st, g);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

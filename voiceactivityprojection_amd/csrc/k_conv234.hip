@@ -398,13 +398,11 @@ hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
   const int ntb = (a.M + 255) / 256, ntiles = ntb * S;
   // persistent: at most one workgroup per CU free beside the recurrence (a.grid_cap, 0 = all CUs);
   // one tile per workgroup when the tiles fit in one round anyway
-  // Default: one tile per workgroup.  The persistent form (VAP_CONVK4_PERSIST=1, workgroups capped at
-  // a.grid_cap) measured slower in the bench (conv2..4 1.75 vs 1.50 ms per step): its next tile's
-  // block 0 waits for the epilogue stores and W(0), and static striding balances worse than the
-  // dispatcher handing tiles to whichever CU frees up.
-  static const bool persist = getenv("VAP_CONVK4_PERSIST") != nullptr;
-  const int cap = persist ? (a.grid_cap > 0 ? a.grid_cap : 256) : ntiles;
-  const dim3 grid(std::min(ntiles, cap));
+  // One tile per workgroup.  The kernel's tile loop also runs persistently (grid capped at the CUs
+  // free beside the recurrence, a.grid_cap), which measured slower in the bench (conv2..4 1.75 vs
+  // 1.50 ms per step): its next tile's block 0 waits for the epilogue stores and W(0), and static
+  // striding balances worse than the dispatcher handing tiles to whichever CU frees up.
+  const dim3 grid(ntiles);
   switch (a.dbg) {
     case 0: hipLaunchKernelGGL(convk4_kernel<0>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
     case 1: hipLaunchKernelGGL(convk4_kernel<1>, grid, dim3(512), 0, st, a, ntb, ntiles); break;

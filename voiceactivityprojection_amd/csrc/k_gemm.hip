@@ -235,12 +235,11 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.K % BK != 0 || g.N % BN != 0 || M <= 0) return hipErrorInvalidValue;
   if (g.norm && g.N != BN) return hipErrorInvalidValue;
   if constexpr (sizeof(T) == 2) {
-    static const bool v1 = getenv("VAP_GEMM_V1") != nullptr;
     const bool aligned = !(g.lda % 8 || g.a_seq_stride % 8 || g.ldc % 4 || g.c_seq_stride % 4 ||
                            (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)));
     // The kernel choice must not depend on M: a clip's outputs are then bit-identical whatever
     // batch (or shard of a batch) it runs in -- the 128-row kernel accumulates in another order.
-    if (!v1 && aligned) return launch_gemm2<TOut>(g, st);
+    if (aligned) return launch_gemm2<TOut>(g, st);
   }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);

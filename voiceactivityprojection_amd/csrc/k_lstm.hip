@@ -454,11 +454,6 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   const bool valid = seq < S;
   const int u0 = 128 * p + 16 * w + 4 * (lane >> 4);  // this lane's 4 units (rows of the gate tiles)
 
-  if (sync.wave_prio && w < 4) {  // the two waves of a SIMD (w, w + 4) out of step: w's cells beside w+4's MFMAs
-    if (sync.wave_prio == 1) __builtin_amdgcn_s_setprio(1);
-    else if (sync.wave_prio == 2) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(3);
-  }
   chunk16 wa[P_NF];  // fragment f = g*8 + kk: rows g*256 + 128p + 16w + (lane&15), k = 32kk + 8(lane>>4) + e
   const chunk16* wsrc = wp + (int64_t)(p * P_NW + w) * P_NF * 64 + lane;
 #pragma unroll
@@ -558,7 +553,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   // overwritten at step 1, after the partner consumed step 0, i.e. after it read this granule) and
   // reads the partner lane's; a timed-out handshake keeps write-through and sets the error word.
   bool xl2 = sync.xplain > 0;  // VAP_LSTM_XPLAIN: 1 plain stores always, -1 never, 0 (default) by handshake
-  if (sync.xplain == 0 && !sync.xnowait) {
+  if (sync.xplain == 0) {
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
     const uint32_t htag = tag_base - 1u;
@@ -601,8 +596,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
     const uint32_t xo_rem = x_rem + (uint32_t)(((t - 1) & 1) * 512 * 16);
     u32x4 xv = {0u, 0u, 0u, 0u};
     if (t > 0) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(xv) : "v"(xo_rem), "s"(xr) : "memory");
-    gload(gc, sync.xnostore > 1 ? 0 : t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
-    // (xnostore 2: diagnostics, every step reloads row 0)
+    gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const chunk16 hf = hfrag(kown + q);
@@ -615,7 +609,7 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // P landed (G may still be in flight)
       const uint32_t want = tag_base + (uint32_t)(t - 1);
       uint64_t t0 = 0;
-      while (!dead && !sync.xnowait && !__all(xv[1] == want && xv[3] == want)) {
+      while (!dead && !__all(xv[1] == want && xv[3] == want)) {
         if (!t0) {
           t0 = __builtin_amdgcn_s_memrealtime();
         } else if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
@@ -651,9 +645,8 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
       asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 2" ::"v"(xo), "v"(xoff), "s"(xr) : "memory");
     // (the s_nops: a VALU write of a store's data VGPRs right after a dwordx3/x4 store is a hazard the
     // compiler does not see through inline asm)
-    if (!sync.xnostore)  // (xnostore: timing diagnostics only, the outputs are garbage)
-      asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
-                   "s"(orsc) : "memory");
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
+                 "s"(orsc) : "memory");
     hput(u0, hp);  // own units of h_t (the own-unit reads of this step retired before B1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // B2: own h_t visible to every wave
@@ -848,14 +841,8 @@ hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16*
   const char* xpe = getenv("VAP_LSTM_XPLAIN");  // read per launch (tests switch it)
   const int xplain = xpe ? atoi(xpe) : 0;
   sy.xplain = xplain;
-  static const int xnowait = getenv("VAP_LSTM_XNOWAIT") ? atoi(getenv("VAP_LSTM_XNOWAIT")) : 0;  // timing diagnostics only
-  sy.xnowait = xnowait;
   static const int hot = getenv("VAP_LSTM_HANDOFF") ? atoi(getenv("VAP_LSTM_HANDOFF")) : 0;  // diagnostics
   sy.handoff_trace = hot;
-  static const int wprio = getenv("VAP_LSTM_PRIO") ? atoi(getenv("VAP_LSTM_PRIO")) : 0;
-  sy.wave_prio = wprio;
-  static const int xnostore = getenv("VAP_LSTM_XNOSTORE") ? atoi(getenv("VAP_LSTM_XNOSTORE")) : 0;  // diagnostics
-  sy.xnostore = xnostore;
   static const int st0 = getenv("VAP_LSTM_STAMP_T0") ? atoi(getenv("VAP_LSTM_STAMP_T0")) : 100;
   sy.stamp_t0 = st0;
   const int groups = (S + NS - 1) / NS;

@@ -53,7 +53,6 @@ struct vap_handle {
   // micro-batch pipeline: side streams for the LSTM recurrences + events
   static constexpr int NSIDE = 3, MAXMB = 16;
   int microbatches = 4;
-  double tc_edge = 0.0;             // time chunks: first / last chunk fraction of the frames (0: even split)
   // forward: front-end / back-end boundaries (cumulative frame fractions, VAP_TC_FE / VAP_TC_BE;
   // "" = the even time_chunks split for both)
   // (the pair-split recurrence ends well before the caller stream's work: two back-end chunks, the
@@ -61,7 +60,6 @@ struct vap_handle {
   // (seven growing front-end pieces started the recurrence sooner in single-forward traces but
   // measured 3.5 % slower in the back-to-back bench: kept as VAP_TC_FE=0.05,0.12,0.2,0.3,0.42,0.56,0.72)
   std::vector<double> tc_fe{0.1, 0.27, 0.48, 0.72}, tc_be{0.64};
-  std::vector<double> tc_split;     // VAP_TC_SPLIT: explicit relative chunk sizes
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
@@ -71,11 +69,7 @@ struct vap_handle {
   // of workgroups shares the chip with the other kernel (VAP_FE_STREAMS=1: all on the caller stream)
   // (VAP_FE_STREAMS=2, session 4: within 1 % of one stream in the bench, +1.5 % in back-to-back
   // forwards without per-launch timing events; one stream keeps each kernel's events clean)
-  hipStream_t fe_stream = nullptr;
   int fe_streams = 2;
-  bool fe_first_serial = false;
-  int fe_gate = 0;  // VAP_FE_GATE: see conv_rows
-  bool fe_align = true;  // VAP_FE_ALIGN=0: conv1..3 ranges per piece exactly what its conv4 rows need
   hipEvent_t mb_ev[MAXMB] = {};
   hipEvent_t fork_ev[MAXMB] = {};
   int fork_next = 0;
@@ -90,12 +84,10 @@ struct vap_handle {
   unsigned* err_dev = nullptr;
   // bf16 recurrence: split over workgroup pairs (k_lstm.hip lstm_pair_kernel, two CUs per 16 sequences)
   // conv2..4 on the slab-staged k4 s2 kernel (k_conv234.hip); VAP_CONVK4=0: implicit GEMMs on gemm2
-  bool convk4 = true;
   // time-chunked back end: each layer's block kernel also computes the next layer's LN + Q/K/V (and
   // cross K/V) from the rows it holds, one launch and one read of x less per layer transition
   // (VAP_BLOCK_FUSE=0: separate lnproj launches)
   bool block_fuse = true;
-  bool fe_join_late = true;  // VAP_FE_JOIN=0: the back end waits for the whole front-end stream
   int be_split = 2;  // VAP_BE_SPLIT=1: the time-chunked back end on the caller stream only (tc_back_end)
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
@@ -107,9 +99,7 @@ struct vap_handle {
   unsigned epoch = 0;
   unsigned done_expect[MAXMB] = {};
   bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
-  bool persistent_lstm = true;  // VAP_PERSISTENT_LSTM=0: one LSTM launch per range on the side streams
   int time_chunks = 4;          // VAP_TIME_CHUNKS (bf16, 1-layer LSTM): pipeline the forward along time
-  int tc_streams = 1;           // VAP_TC_STREAMS=2: back ends on their own stream (measured: no gain, kernels fill the GPU)
   bool use_time_chunks() const {
     return dims.precision == VAP_PRECISION_BF16 && dims.lstm_layers == 1 && time_chunks >= 2 && !dims.mono;
   }
@@ -121,11 +111,10 @@ struct vap_handle {
     // side[1] doubles as the front-end stream of the time-pipelined forward (a stream of its own
     // would share one of the process's GPU_MAX_HW_QUEUES hardware queues with another, which
     // measured slower); VAP_FE_PRIO=1 creates it with the highest priority
-    static const int fe_prio = getenv("VAP_FE_PRIO") ? atoi(getenv("VAP_FE_PRIO")) : 1;
     int prio_lo = 0, prio_hi = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) return VAP_ERR_HIP;
     for (int i = 0; i < NSIDE; ++i)
-      if (hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, i == 1 && fe_prio ? prio_hi : prio_lo) != hipSuccess)
+      if (hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, i == 1 ? prio_hi : prio_lo) != hipSuccess)
         return VAP_ERR_HIP;
     for (int i = 0; i < MAXMB; ++i) {
       if (hipEventCreateWithFlags(&mb_ev[i], hipEventDisableTiming) != hipSuccess) return VAP_ERR_HIP;
@@ -165,7 +154,6 @@ struct vap_handle {
       if (err_host) (void)hipHostFree(err_host);
       if (xbuf) (void)hipFree(xbuf);
       for (auto& st : side) (void)hipStreamDestroy(st);
-      if (fe_stream && fe_stream != side[1]) (void)hipStreamDestroy(fe_stream);
       for (int i = 0; i < MAXMB; ++i) {
         (void)hipEventDestroy(mb_ev[i]);
         (void)hipEventDestroy(fork_ev[i]);
@@ -786,7 +774,7 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     const std::string c = std::to_string(i + 1);
     Timed tm(h, i == 0 ? VAP_K_CONV1 : VAP_K_CONV234, st);
     if constexpr (sizeof(T) == 2) {
-      if (i >= 1 && h->convk4) {
+      if (i >= 1) {
         ConvK4Args ca{(const bf16*)ins[i], in_ss[i], (int)(in_ss[i] / D), (const bf16*)h->W<T>("conv" + c + "_ks"),
                       h->P(g + ".conv" + c + ".bias"), h->P(g + ".batchNorm" + c + ".weight"),
                       h->P(g + ".batchNorm" + c + ".bias"), (bf16*)(Xs[i] + D), ss[i], (int)L[i + 1]};
@@ -1115,31 +1103,13 @@ struct TcSched {
   int nbe = 1;                          // back-end chunks: chunk k covers recurrence chunks
   int be_end[vap_handle::MAXMB + 1]{};  // [be_end[k-1], be_end[k]) (be_end[-1] = 0)
 };
-// Chunk sizes: the step is bounded by the caller-stream work AND by the chain "front end of chunk 0
-// -> whole recurrence -> back end of the last chunk", so the first and last chunks are short (edge
-// fraction h->tc_edge of the frames each, >= 32 frames) and the middle ones share the rest evenly.
-// VAP_TC_SPLIT="w0,w1,.." sets explicit relative chunk sizes instead.
+// Even chunks (the fallback of tc_schedule_split for short clips or custom chunk counts).
 TcSched tc_schedule(const vap_handle* h, const Plan& p) {
   TcSched t;
   const int T_ = p.T;
   t.nch = std::min(h->time_chunks, vap_handle::MAXMB);
   t.nch = std::max(1, std::min(t.nch, T_ / 32));  // chunks of at least 32 frames
-  std::vector<double> wt;
-  if (!h->tc_split.empty()) {
-    for (double v : h->tc_split) wt.push_back(v);
-    if ((int)wt.size() > std::min(vap_handle::MAXMB, T_ / 32)) wt.clear();
-  }
-  if (wt.empty()) {
-    wt.assign(t.nch, 1.0);
-    if (t.nch >= 3 && h->tc_edge > 0.0) {
-      const double e = std::max(h->tc_edge, 32.0 / T_);
-      const double mid = (1.0 - 2 * e) / (t.nch - 2);
-      if (mid * T_ >= 32) {
-        for (int c = 0; c < t.nch; ++c) wt[c] = (c == 0 || c == t.nch - 1) ? e : mid;
-      }
-    }
-  }
-  t.nch = (int)wt.size();
+  const std::vector<double> wt(t.nch, 1.0);
   double tot = 0;
   for (double v : wt) tot += v;
   double acc = 0;
@@ -1259,11 +1229,11 @@ int heads_tc(vap_handle* h, const Plan& p, unsigned char* ws, int f0, int f1, fl
 // side[1] (its join event passed in), per-chunk heads, whole clips in each half, and no back-end class
 // timed (vap_timing brackets one stream's launches).
 static int be_split_ways(const vap_handle* h, const Plan& p, bool fe_on_side1) {
-  if (h->be_split < 2 || !fe_on_side1 || h->fe_stream || !h->heads_chunked || h->dims.cross_layers <= 0 || p.B < 2)
+  if (h->be_split < 2 || !fe_on_side1 || !h->heads_chunked || h->dims.cross_layers <= 0 || p.B < 2)
     return 1;
   const int tc = h->timing_cls;
   if (tc == VAP_K_DOWNSAMPLE || tc == VAP_K_TR_GEMM || tc == VAP_K_ATTN || tc == VAP_K_HEADS) return 1;
-  return 2;
+  return std::min(std::min(h->be_split, 3), p.B);
 }
 
 // Back end of the time-chunked forward: per chunk, wait for the recurrence (done[c]), downsample,
@@ -1278,25 +1248,24 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
   const int64_t t1 = (int64_t)T_ * D;
   T* Hf = (T*)(ws + p.H0);
   float* X = (float*)(ws + p.X);
-  // with tc_streams >= 2 the back end runs on its own stream so chunk c's transformer may overlap the
   // later chunks' front ends; the LSTM hand-off orders them
-  hipStream_t bst = h->tc_streams >= 2 ? h->side[1] : st;
-  if (bst != st) {
-    hipEvent_t fk = h->next_fork_event();
-    HIPCHK(hipEventRecord(fk, st));
-    HIPCHK(hipStreamWaitEvent(bst, fk, 0));
-  }
+  const hipStream_t bst = st;
   // be_split = 2 (sequence halves on two streams: the caller's and the front-end stream, which joins
   // once the last front-end piece is done): each launch's last partial round of workgroups, and the
   // attention (VALU / MFMA) beside the row kernels (HBM), share the chip with the other half's launches
   const int nsp = be_split_ways(h, p, fe_join != nullptr && !kernel_expect && bst == st);
+  if (nsp > 2) {  // the third group's stream follows everything the caller stream has queued so far
+    hipEvent_t fk = h->next_fork_event();
+    HIPCHK(hipEventRecord(fk, st));
+    HIPCHK(hipStreamWaitEvent(h->side[2], fk, 0));
+  }
   int rc;
   for (int k = 0; k < t.nbe; ++k) {
     const int c = t.be_end[k] - 1;  // the last recurrence chunk of back-end chunk k
     const int f0 = t.fb[k ? t.be_end[k - 1] : 0], f1 = t.fb[c + 1];
    for (int g = 0; g < nsp; ++g) {
     const int sq0 = nsp == 1 ? 0 : (p.B * g / nsp) * 2, sq1 = nsp == 1 ? S : (p.B * (g + 1) / nsp) * 2;
-    const hipStream_t bs = g == 0 ? bst : h->side[1];
+    const hipStream_t bs = g == 0 ? bst : h->side[g];
     if (kernel_expect)  // captured streaming push: the hand-off as a kernel (graph-capturable)
       HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bs));
     else
@@ -1338,14 +1307,15 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     fe_join = h->next_fork_event();
     HIPCHK(hipEventRecord(fe_join, h->side[1]));
   }
+  if (nsp > 2) {
+    hipEvent_t j2 = h->next_fork_event();
+    HIPCHK(hipEventRecord(j2, h->side[2]));
+    HIPCHK(hipStreamWaitEvent(st, j2, 0));
+  }
   if (fe_join) HIPCHK(hipStreamWaitEvent(st, fe_join, 0));
   if (!join) return VAP_OK;  // (captured push: the caller joins outside the graph)
   HIPCHK(hipEventRecord(h->mb_ev[0], h->side[0]));  // join: the LSTM launch has fully retired
   HIPCHK(hipStreamWaitEvent(st, h->mb_ev[0], 0));
-  if (bst != st) {
-    HIPCHK(hipEventRecord(h->mb_ev[1], bst));
-    HIPCHK(hipStreamWaitEvent(st, h->mb_ev[1], 0));
-  }
   return VAP_OK;
 }
 
@@ -1378,7 +1348,7 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     // stopped: the rows past what this piece needs are pulled forward from the next piece, not
     // extra work, and only the first and the last piece launch a partial tile per sequence
     for (int i = 2; i >= 0; --i) {
-      if (h->fe_align && a4 > 0) {
+      if (a4 > 0) {
         const int64_t need = std::min(L[i + 1], 2 * b[i + 1] + 1);
         b[i] = std::min(L[i + 1], std::max(need, a[i] + (need - a[i] + 255) / 256 * 256));
       }
@@ -1394,45 +1364,23 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
   }
   if (done_lv)
     for (int i = 0; i < 3; ++i) done_lv[i] = b[i];
-  hipStream_t st0 = st;
   if (st2) {
     hipEvent_t fk = h->next_fork_event();
     HIPCHK(hipEventRecord(fk, st));
     HIPCHK(hipStreamWaitEvent(st2, fk, 0));
     st = st2;
   }
-  // VAP_FE_GATE=g (1..3): the caller stream's next launch (the next piece's conv01) waits until
-  // conv(g+1) of this piece is done, so it does not take the CUs those launches need first
-  auto gate = [&](int lvl) -> int {
-    if (st2 && h->fe_gate == lvl) {
-      hipEvent_t gk = h->next_fork_event();
-      HIPCHK(hipEventRecord(gk, st2));
-      HIPCHK(hipStreamWaitEvent(st0, gk, 0));
-    }
-    return VAP_OK;
-  };
+
   for (int i = 1; i < 4; ++i) {  // conv2..4 (encoder_components.py:100-103)
     const std::string cs = std::to_string(i + 1);
-    if (i > 1 && gate(i - 1)) return VAP_ERR_HIP;
     if (a[i] >= b[i]) continue;
     Timed tm(h, VAP_K_CONV234, st);
-    if (h->convk4) {
-      ConvK4Args ca{Xs[i - 1] + a[i] * 2 * D, ss[i - 1], (int)(ss[i - 1] / D - 2 * a[i]), (const bf16*)h->W<T>("conv" + cs + "_ks"),
-                    h->P(g + ".conv" + cs + ".bias"), h->P(g + ".batchNorm" + cs + ".weight"),
-                    h->P(g + ".batchNorm" + cs + ".bias"), Xs[i] + D + a[i] * D, ss[i], (int)(b[i] - a[i])};
-      ca.grid_cap = conv_grid_cap(h, S);
-      HIPCHK(launch_convk4(ca, S, st));
-      continue;
-    }
-    GemmArgs ga = gargs(Xs[i - 1] + a[i] * 2 * D, 2 * D, ss[i - 1], h->W<T>("conv" + cs), 4 * D, D,
-                        h->P(g + ".conv" + cs + ".bias"), (int)(b[i] - a[i]), S, Xs[i] + D + a[i] * D, D, ss[i]);
-    ga.norm = 1;
-    ga.act = 1;
-    ga.gamma = h->P(g + ".batchNorm" + cs + ".weight");
-    ga.beta = h->P(g + ".batchNorm" + cs + ".bias");
-    HIPCHK(gemm<T>(ga, st, false));
+    ConvK4Args ca{Xs[i - 1] + a[i] * 2 * D, ss[i - 1], (int)(ss[i - 1] / D - 2 * a[i]), (const bf16*)h->W<T>("conv" + cs + "_ks"),
+                  h->P(g + ".conv" + cs + ".bias"), h->P(g + ".batchNorm" + cs + ".weight"),
+                  h->P(g + ".batchNorm" + cs + ".bias"), Xs[i] + D + a[i] * D, ss[i], (int)(b[i] - a[i])};
+    ca.grid_cap = conv_grid_cap(h, S);
+    HIPCHK(launch_convk4(ca, S, st));
   }
-  if (gate(3)) return VAP_ERR_HIP;
   // gate projections of rows [a4, b4) into ring slots (r + gx_off) mod L4: at most two pieces
   Timed tm(h, VAP_K_LSTM_PROJ, st);
   for (int64_t r = a4; r < b4;) {
@@ -1471,33 +1419,23 @@ int run_forward_tc(vap_handle* h, const Plan& p, const float* wav, int64_t N, fl
   // (timing mode, vap_timing, for a class that would run on the front-end stream: one stream, so its
   // events bracket only its own kernels; the bench times conv1, whose launches stay on st)
   const bool fe_timed = h->timing_serial || h->timing_cls == VAP_K_CONV234 || h->timing_cls == VAP_K_LSTM_PROJ;
-  hipStream_t fst = h->fe_streams < 2 || fe_timed ? nullptr
-                    : h->fe_stream                   ? h->fe_stream
-                    : h->tc_streams < 2              ? h->side[1]
-                                                     : nullptr;
+  hipStream_t fst = h->fe_streams < 2 || fe_timed ? nullptr : h->side[1];
   for (int c = 0; c < t.nch; ++c) {  // front end, piece by piece (a piece ends at a front-end boundary)
     if (!t.fe_pub[c]) continue;
-    // VAP_FE_FIRST_SERIAL=1: the first piece all on st (its conv2..4 do not share the chip with the
-    // second piece's conv01, so the recurrence starts earlier)
-    const bool ser = h->fe_first_serial && done_rows == 0;
-    if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st, 0, ser ? nullptr : fst, done_lv))) return rc;
+    if ((rc = conv_rows(h, p, wav, N, ws, GX, done_rows, t.seq_end[c], st, 0, fst, done_lv))) return rc;
 
     done_rows = t.seq_end[c];
     for (; published <= c; ++published)
       if (published != h->test_drop_ready)
-        HIPCHK(hipStreamWriteValue32(fst && !ser ? fst : st, (void*)(sy.ready + published), sy.epoch, 0));
+        HIPCHK(hipStreamWriteValue32(fst ? fst : st, (void*)(sy.ready + published), sy.epoch, 0));
   }
   // join: anything after the forward on st follows the whole front end.  The back end itself waits
   // only for the recurrence (done[] flags), so its first chunk may start while the front-end stream
-  // still runs the last piece's conv2..4 and gate projections (VAP_FE_JOIN=0: join before it)
+  // still runs the last piece's conv2..4 and gate projections
   hipEvent_t jn = nullptr;
   if (fst) {
     jn = h->next_fork_event();
     HIPCHK(hipEventRecord(jn, fst));
-    if (!h->fe_join_late) {
-      HIPCHK(hipStreamWaitEvent(st, jn, 0));
-      jn = nullptr;
-    }
   }
   return tc_back_end(h, p, t, sy, ws, logits, vadl, st, nullptr, true, jn);
 }
@@ -1576,7 +1514,7 @@ int run_forward(vap_handle* h, const float* wav, int B, int64_t N, float* logits
   }
   if ((rc = h->ensure_streams())) return rc;
   if constexpr (sizeof(T) == 2) {
-    if (h->wait_value && h->persistent_lstm && persistent_fits(h, S)) {
+    if (h->wait_value && persistent_fits(h, S)) {
       // One persistent LSTM launch on a side stream covers every range: its workgroups start as
       // each range's gate projection lands (ready flag written by this stream) and publish done
       // counters the back ends wait on.  No per-range launches, so no range queues behind another
@@ -1813,7 +1751,7 @@ int stream_push(vap_stream* s, const float* hop_audio, float* logits, float* vad
   const int S = p.S;
   const int nxt = 1 - s->cur;
   const int64_t W = s->W, hop = s->hop, L4 = p.L[4];
-  if (s->graph && s->reuse && s->pushes > 0 && s->keep1 > s->keep0 && h->timing_cls == 0 && h->tc_streams < 2)
+  if (s->graph && s->reuse && s->pushes > 0 && s->keep1 > s->keep0 && h->timing_cls == 0)
     return stream_push_graph(s, hop_audio, logits, vadl, st);
   // roll: window[:, :W-hop] = old window[:, hop:], window[:, W-hop:] = the new samples
   HIPCHK(hipMemcpy2DAsync(s->win[nxt], W * sizeof(float), s->win[s->cur] + hop, W * sizeof(float),
@@ -1914,19 +1852,11 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   h->dims = *dims;
   if (const char* e = getenv("VAP_MICROBATCHES")) h->microbatches = atoi(e);
   if (const char* e = getenv("VAP_HEADS_CHUNKED")) h->heads_chunked = atoi(e) != 0;
-  if (const char* e = getenv("VAP_PERSISTENT_LSTM")) h->persistent_lstm = atoi(e) != 0;
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
-  if (const char* e = getenv("VAP_TC_STREAMS")) h->tc_streams = atoi(e);
   if (const char* e = getenv("VAP_FE_STREAMS")) h->fe_streams = atoi(e);
-  if (const char* e = getenv("VAP_FE_ALIGN")) h->fe_align = atoi(e) != 0;
-  if (const char* e = getenv("VAP_FE_FIRST_SERIAL")) h->fe_first_serial = atoi(e) != 0;
-  if (const char* e = getenv("VAP_FE_GATE")) h->fe_gate = atoi(e);
-  if (const char* e = getenv("VAP_TC_EDGE")) h->tc_edge = atof(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
-  if (const char* e = getenv("VAP_CONVK4")) h->convk4 = atoi(e) != 0;
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
-  if (const char* e = getenv("VAP_FE_JOIN")) h->fe_join_late = atoi(e) != 0;
   if (const char* e = getenv("VAP_BE_SPLIT")) h->be_split = atoi(e);
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
@@ -1942,17 +1872,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   };
   if (const char* e = getenv("VAP_TC_FE")) parse_list(e, h->tc_fe);
   if (const char* e = getenv("VAP_TC_BE")) parse_list(e, h->tc_be);
-  if (const char* e = getenv("VAP_TC_SPLIT")) {
-    std::string v = e;
-    size_t a = 0;
-    while (a < v.size()) {
-      size_t b = v.find(',', a);
-      if (b == std::string::npos) b = v.size();
-      const double x = atof(v.substr(a, b - a).c_str());
-      if (x > 0) h->tc_split.push_back(x);
-      a = b + 1;
-    }
-  }
+
   if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
   add_schema(h);

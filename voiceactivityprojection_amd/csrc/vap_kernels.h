@@ -119,9 +119,6 @@ struct LstmSync {
   int xplain = 0;       // lstm_pair: exchange stores with the default policy even across XCDs (experiment; the
                         // XCC-id handshake picks that policy by itself when both halves share an XCD)
   int stamp_t0 = 100;   // lstm_pair<ST>: first of the 4 stamped steps (VAP_LSTM_STAMP_T0)
-  int xnostore = 0;     // lstm_pair: skip the h row stores (timing diagnostics; outputs are garbage)
-  int xnowait = 0;      // lstm_pair: do not wait for the partner (timing diagnostics; outputs are garbage)
-  int wave_prio = 0;  // lstm_pair (VAP_LSTM_PRIO): waves 0-3 at this s_setprio level, 4-7 at 0 (experiment)
   int handoff_trace = 0;  // lstm_pair (VAP_LSTM_HANDOFF=1): workgroup 0 records s_memrealtime around each hand-off
 };
 // diagnostics: [0] launch start, then per time chunk c: [1 + 3c] ready wait begins, [2 + 3c] ready seen,
