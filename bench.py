@@ -97,6 +97,8 @@ def parse_args(argv=None):
                     help="outputs shipped to rank 0: all six probs() outputs, or p_now/p_future/vad/H")
     # CPU rehearsal of the launcher / gather path (tests/test_bench_launcher.py): gloo ranks on the host
     # with a stub step that writes rank-tagged outputs; no GPU, no engine
+    ap.add_argument("--roofline-events", type=int, default=-1,
+                    help="timed steps (the last ones) whose dominant-kernel launches carry HIP events (-1: all)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -246,14 +248,18 @@ def run_rank(args) -> int:
         iso_tot, iso_cnt = ctypes.c_double(), ctypes.c_int()
         N.check(lib.vap_timing_read(h, ctypes.byref(iso_tot), ctypes.byref(iso_cnt)))
         model.synchronize()
-        N.check(lib.vap_timing(h, N.KERNEL_CLASS[dominant]))
+    ev_from = 0 if args.roofline_events < 0 else max(0, args.steps - args.roofline_events)
+    if not args.stub and ev_from > 0:
+        N.check(lib.vap_timing(h, 0))  # events only from step ev_from on
 
     # timed region: K steps (+ their gathers), HIP events around every launch of the dominant class
     if dist:
         tdist.barrier()
     device_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if not args.stub and ev_from > 0 and i == ev_from:
+            N.check(lib.vap_timing(h, N.KERNEL_CLASS[dominant]))
         step()
     drain()
     device_sync()
@@ -305,8 +311,11 @@ def run_rank(args) -> int:
         if gather_info is not None:
             line["gather"] = gather_info
         if not args.stub:
+            ev_steps = args.steps - ev_from  # timed steps whose dominant launches carried events
+            if cnt.value == 0:  # --roofline-events 0: the isolated pass's launches stand in
+                tot, cnt, ev_steps = iso_tot, iso_cnt, 1
             dom_ms_per_launch = tot.value / max(1, cnt.value)
-            launches_per_step = max(1, cnt.value // args.steps)
+            launches_per_step = max(1, cnt.value // max(1, ev_steps))
             flop_per_launch = flops[dominant] / launches_per_step
             achieved = flop_per_launch / (dom_ms_per_launch * 1e-3) / 1e12
             peak = PEAK_TFLOPS[args.precision]
@@ -314,12 +323,12 @@ def run_rank(args) -> int:
             # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
             # by the concurrent LSTM) x the rows of one launch here
             traffic, traffic_src = None, None
-            tp = os.path.join(REPO, "profiles", "r2_traffic_pmc.json")  # the current conv01 kernel (v11)
+            tp = os.path.join(REPO, "profiles", "r3_traffic_pmc.json")  # the current conv01 kernel (v11)
             if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
                 per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
                 rows_per_launch = 2 * B * L[1] / launches_per_step
                 traffic = round(per_row * rows_per_launch / 1e9, 3)
-                traffic_src = "profiles/r2_traffic_pmc.json (GB per launch)"
+                traffic_src = "profiles/r3_traffic_pmc.json (GB per launch)"
             line["roofline"] = {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                                 "traffic_source": traffic_src, "flop_per_launch": flop_per_launch,
@@ -338,7 +347,8 @@ def run_rank(args) -> int:
                                       "persistent side-stream launch overlapped with the caller-stream classes (its "
                                       "time includes waiting for the time chunks); the front end runs on two "
                                       "streams (conv01 of piece k+1 beside conv2..4 + gate projection of piece k), "
-                                      "the back end back to back on the caller's stream")
+                                      "the back end in two clip halves on two streams; a back-end class is timed in "
+                                      "a forward with the back end on one stream")
             line["model_tflops_per_s"] = round(sum(flops.values()) * args.steps * world / el / 1e12, 2)
         if world == 1 and not args.no_cpu_baseline and not args.stub:
             line["cpu_baseline"] = cpu_baseline(args.seconds, sd_np)

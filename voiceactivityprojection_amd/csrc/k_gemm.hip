@@ -239,7 +239,7 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
                            (g.add && (g.ld_add % 4 || g.add_seq_stride % 4)));
     // The kernel choice must not depend on M: a clip's outputs are then bit-identical whatever
     // batch (or shard of a batch) it runs in -- the 128-row kernel accumulates in another order.
-    if (aligned) return launch_gemm2<TOut>(g, st);
+    if (aligned && !g.small_tiles) return launch_gemm2<TOut>(g, st);
   }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);

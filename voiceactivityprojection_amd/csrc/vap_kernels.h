@@ -24,6 +24,9 @@ struct GemmArgs {
   // pair-recurrence layout (gx_pair_block): a tile is 16 time steps x 16 sequences (of sequences
   // c_s0 + 16k ..), row t of sequence s lands in ring slot (c_t0 + t) mod c_tn; ldc / c_seq_stride unused
   int c_pair = 0, c_s0 = 0, c_t0 = 0, c_tn = 0;
+  // small_tiles = 1: the 128-row register-staged kernel even for bf16 (more workgroups for short launches;
+  // chosen by the caller per call site, never by M, so outputs stay batch-invariant)
+  int small_tiles = 0;
 };
 
 template <typename T, typename TOut>
