@@ -97,7 +97,9 @@ def parse_args(argv=None):
                     help="outputs shipped to rank 0: all six probs() outputs, or p_now/p_future/vad/H")
     # CPU rehearsal of the launcher / gather path (tests/test_bench_launcher.py): gloo ranks on the host
     # with a stub step that writes rank-tagged outputs; no GPU, no engine
-    ap.add_argument("--roofline-events", type=int, default=-1,
+    # HIP events around every dominant-kernel launch of EVERY timed step cost ~7 % of the step (each event
+    # pair splits the two front-end streams' overlap); the last timed step carries them by default
+    ap.add_argument("--roofline-events", type=int, default=1,
                     help="timed steps (the last ones) whose dominant-kernel launches carry HIP events (-1: all)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
@@ -332,7 +334,8 @@ def run_rank(args) -> int:
             line["roofline"] = {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                                 "traffic_source": traffic_src, "flop_per_launch": flop_per_launch,
-                                "ms_per_launch": round(dom_ms_per_launch, 4), "launches": cnt.value}
+                                "ms_per_launch": round(dom_ms_per_launch, 4), "launches": cnt.value,
+                                "event_steps": ev_steps}
             if dominant in ("conv1", "conv234", "lstm_proj"):
                 iso_ms = iso_tot.value / max(1, iso_cnt.value)
                 iso_ach = flop_per_launch / (iso_ms * 1e-3) / 1e12

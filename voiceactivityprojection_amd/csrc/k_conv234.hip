@@ -107,16 +107,6 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
   // (logical chunk held at physical chunk lane%4) x 8 elements; tile rows start at input row 2 t0.
   // Recomputed from an opaque copy of the lane id at each use: hoisted out of the tile loop, these
   // per-lane constants spilled to scratch (and every reload waited for all loads in flight).
-  auto prow = [&](int k) -> uint32_t {
-    const int ln = ck_lane();
-    int wo = w;
-    asm volatile("" : "+s"(wo));
-    const int q = k == 4 && wo >= 2 ? wo + 24 : wo + 8 * k;
-    const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
-    const int hr = 16 * p + (ln >> 2);
-    const int c = ((ln & 3) - (hr >> 2)) & 3;
-    return (uint32_t)(((2 * hr + hb) << 8) | (c * 8));
-  };
   struct TileSrc {
     const bf16* in;  // sequence base
     int t0;          // first output row
@@ -125,28 +115,34 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
     s_ = tl / ntb;
     return TileSrc{a.in + (int64_t)s_ * a.in_seq_stride, (tl - s_ * ntb) * 256};
   };
-  // Both the slab DMA and the W loads are inline asm with hand-counted waits: the compiler treats a
-  // global_load_lds as an LDS write that may alias every later ds_read and put vmcnt(0) before each
-  // block's first MFMA, draining the two-block-deep DMA stream.  Per block the wave issues, in order,
-  // W(CB+1) (8 loads) then DMA(CB+2) (5 pieces); at the start of block CB, vmcnt(5) leaves only
-  // DMA(CB+1) in flight, so W(CB) and DMA(CB) have landed.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  auto dma1 = [&](const TileSrc& ts, int cb, int sl, int k) {
-    {
-      const int q = piece(k);
-      const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
-      const uint32_t pr = prow(k);
-      const int row = min(2 * ts.t0 + (int)(pr >> 8), a.in_rows - 1);  // rows past the range feed no stored output
-      const bf16* src = ts.in + (row * 256 + (int)(pr & 255u) + cb * 32);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(sl * CK_SLAB + hb * CK_HALF + p * 1024));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-    }
+  // DMA sources through a buffer resource per tile (base: the tile's first input row 2 t0; rows past
+  // the sequence's readable rows read as zero -- they feed no stored output).  The lane's part of a
+  // piece's source offset is the same for every piece: lane -> (row 2 (lane >> 2) of the piece's
+  // 16 half-rows, logical chunk ((lane & 3) - (lane >> 4)) & 3 at physical chunk lane & 3: the swizzle
+  // chunk' = chunk + row/4 only sees row bits the piece base does not change); the piece, half and
+  // channel block are one scalar.  (Per-piece address math on the VALU was ~25 instructions per
+  // piece inside the MFMA stream.)
+  auto tile_rsrc = [&](const TileSrc& ts) {
+    return make_rsrc(ts.in + (int64_t)2 * ts.t0 * 256, (uint32_t)max(0, a.in_rows - 2 * ts.t0) * 512u);
   };
-  auto dma = [&](const TileSrc& ts, int cb, int sl) {
+  auto dlane = [&]() -> uint32_t {
+    const int ln = ck_lane();
+    return (uint32_t)((ln >> 2) * 1024 + (((ln & 3) - (ln >> 4)) & 3) * 16);
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  auto dma1 = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t dl, int cb, int sl, int k) {
+    const int q = piece(k);
+    const int hb = q >= CK_PIECES / 2, p = q - hb * (CK_PIECES / 2);
+    const uint32_t po = __builtin_amdgcn_readfirstlane((uint32_t)(((32 * p + hb) * 256 + cb * 32) * 2));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(sl * CK_SLAB + hb * CK_HALF + p * 1024));
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(dl + po), "s"(rs), "s"(dst) : "memory");
+  };
+  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, int cb, int sl) {
+    const uint32_t dl = dlane();
 #pragma unroll
-    for (int k = 0; k < 5; ++k) dma1(ts, cb, sl, k);
+    for (int k = 0; k < 5; ++k) dma1(rs, dl, cb, sl, k);
   };
   // ---- W fragments of block cb: [tap j][k half kh] (A of the 32x32x16: channel 32w + lane%32)
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.W, 32 * 256 * 64);
@@ -185,6 +181,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
 
   int s;
   TileSrc cur = tile_src(tile, s);
+  __amdgpu_buffer_rsrc_t crs = tile_rsrc(cur);
   // Two sets of W fragments (block CB in set CB % 2).  Issue order per wave and block CB: W(CB+1)
   // (8 loads) then DMA(CB+2) (5 pieces) at the block start, so at the start of block CB, vmcnt(5)
   // leaves only DMA(CB+1) in flight: W(CB) and DMA(CB) have landed.  Across tiles: blocks 6 / 7 issue
@@ -198,8 +195,8 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
 #pragma unroll
     for (int f = 0; f < 8; ++f) wload1(wlo, 0, f, W[0][f]);
   }
-  dma(cur, 0, 0);
-  dma(cur, 1, 1);
+  dma(crs, 0, 0);
+  dma(crs, 1, 1);
 
   // G fragment (tap j, k half kh, row tile i) -> half j%2, rows 32i + lane%32 + j/2.  The swizzle
   // depends on the lane, j/2 and kh only (32i is a multiple of 4 rows), so a block reads through four
@@ -218,6 +215,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
     const bool has_next = nxt < ntiles;
     int sn = 0;
     const TileSrc nx = tile_src(has_next ? nxt : tile, sn);
+    const __amdgpu_buffer_rsrc_t nrs = tile_rsrc(nx);
     const int t0 = cur.t0;
     acc_init();
     auto block = [&](auto cbc) {
@@ -250,6 +248,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
       asm volatile("s_barrier" ::: "memory");  // every wave's pieces of CB landed; slot (CB+2)%3 fully read
       __builtin_amdgcn_sched_barrier(0);
       stamp();
+      const uint32_t dl = dlane();
       if constexpr (CB + 1 < 8) {
         const uint32_t wlo = wlane();
 #pragma unroll
@@ -273,8 +272,8 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
         const int m = n + GA;
         if (m < 64) gf[m & GA] = gread(m >> 4, (m >> 3) & 1, m & 7);
         if ((n & 7) == 4 && n < 40) {
-          if constexpr (CB + 2 < 8) dma1(cur, CB + 2, sl2, n >> 3);
-          else if (has_next) dma1(nx, CB - 6, sl2, n >> 3);
+          if constexpr (CB + 2 < 8) dma1(crs, dl, CB + 2, sl2, n >> 3);
+          else if (has_next) dma1(nrs, dl, CB - 6, sl2, n >> 3);
         }
       }
     };
@@ -384,6 +383,7 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
     tile = nxt;
     s = sn;
     cur = nx;
+    crs = nrs;
     gs = gs + 2 >= 3 ? gs - 1 : gs + 2;  // (gs + 8) % 3
   }
 }

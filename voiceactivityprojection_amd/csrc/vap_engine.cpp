@@ -1278,9 +1278,6 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       ga.act = 2;
       ga.gamma = h->P("encoder.downsample.2.ln.weight");
       ga.beta = h->P("encoder.downsample.2.ln.bias");
-#if VAP_DS_SMALL
-      ga.small_tiles = 1;
-#endif
       HIPCHK(gemm<T>(ga, bs, true));
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
