@@ -59,7 +59,10 @@ struct vap_handle {
   // first of 640 frames = 5 full 128-query attention blocks, measured best: 156.2k -> 166.3k audio-s/s)
   // (seven growing front-end pieces started the recurrence sooner in single-forward traces but
   // measured 3.5 % slower in the back-to-back bench: kept as VAP_TC_FE=0.05,0.12,0.2,0.3,0.42,0.56,0.72)
-  std::vector<double> tc_fe{0.1, 0.27, 0.48, 0.72}, tc_be{0.64};
+  // (round 3 with the split back end: five pieces 0.12 / 0.3 / 0.5 / 0.7 / 0.85, +0.8 % over the four
+  // pieces 0.1 / 0.27 / 0.48 / 0.72 in a same-box A/B: a smaller last piece shortens what the recurrence
+  // still has to do after the front end's end)
+  std::vector<double> tc_fe{0.12, 0.3, 0.5, 0.7, 0.85}, tc_be{0.64};
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
