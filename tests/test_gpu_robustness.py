@@ -214,3 +214,20 @@ def test_first_forward_equals_later():
     m.synchronize()
     for k in first:
         assert torch.equal(first[k], later[k]), k
+
+
+def test_back_end_split_bit_identical(monkeypatch):
+    """The time-chunked back end runs in clip groups on two or three streams (VAP_BE_SPLIT, VAP_BE_FRAC:
+    the caller stream's share); every kernel is per sequence and cross attention stays inside a group,
+    so the outputs are bit-identical to the one-stream back end whatever the grouping."""
+    w = _batch(7, 320000, 505)
+    monkeypatch.setenv("VAP_BE_SPLIT", "1")
+    ref = _model().probs(w)
+    for split, frac in (("2", "0.5"), ("2", "0.3"), ("3", "0.5")):
+        monkeypatch.setenv("VAP_BE_SPLIT", split)
+        monkeypatch.setenv("VAP_BE_FRAC", frac)
+        m = _model()
+        out = m.probs(w)
+        m.synchronize()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (split, frac, k)

@@ -91,6 +91,7 @@ struct vap_handle {
   // cross K/V) from the rows it holds, one launch and one read of x less per layer transition
   // (VAP_BLOCK_FUSE=0: separate lnproj launches)
   bool block_fuse = true;
+  double be_frac = 0.5;  // VAP_BE_FRAC: clips of the caller stream's group (two groups)
   int be_split = 2;  // VAP_BE_SPLIT=1: the time-chunked back end on the caller stream only (tc_back_end)
   void* xbuf = nullptr;
   size_t xbuf_bytes = 0;
@@ -1267,7 +1268,14 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     const int c = t.be_end[k] - 1;  // the last recurrence chunk of back-end chunk k
     const int f0 = t.fb[k ? t.be_end[k - 1] : 0], f1 = t.fb[c + 1];
    for (int g = 0; g < nsp; ++g) {
-    const int sq0 = nsp == 1 ? 0 : (p.B * g / nsp) * 2, sq1 = nsp == 1 ? S : (p.B * (g + 1) / nsp) * 2;
+    // clip boundaries of the groups (be_frac: the caller stream's share of two groups)
+    auto cb = [&](int k) {
+      if (k <= 0) return 0;
+      if (k >= nsp) return p.B;
+      if (nsp == 2) return std::min(p.B - 1, std::max(1, (int)(p.B * h->be_frac + 0.5)));
+      return p.B * k / nsp;
+    };
+    const int sq0 = 2 * cb(g), sq1 = 2 * cb(g + 1);
     const hipStream_t bs = g == 0 ? bst : h->side[g];
     if (kernel_expect)  // captured streaming push: the hand-off as a kernel (graph-capturable)
       HIPCHK(launch_wait_geq(sy.done + c, kernel_expect[c], sy.error, bs));
@@ -1861,6 +1869,7 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
   if (const char* e = getenv("VAP_BE_SPLIT")) h->be_split = atoi(e);
+  if (const char* e = getenv("VAP_BE_FRAC")) h->be_frac = atof(e);
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;
