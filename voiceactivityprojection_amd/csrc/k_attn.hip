@@ -205,7 +205,11 @@ VAP_DEV u32x2 tr_read(const unsigned char* p) {
 // software pipeline across key tiles (S_j issued, then the previous tile's P.V, then tile j's softmax
 // beside those MFMAs; V one tile behind K in LDS): 194 VGPRs, 2 waves per SIMD, 0.92 -> 1.03-1.09 ms
 // per bench step (forced to 3 waves: 13 spilled VGPRs, 1.34 ms) -- the third wave per SIMD already
-// hides the softmax behind another wave's MFMAs better than one wave's own pipeline.
+// hides the softmax behind another wave's MFMAs better than one wave's own pipeline.  Key tiles
+// from the diagonal down with the tile max only on the wave's top two tiles (the diagonal tiles set
+// the running max; the older tiles skip 15 v_max3 + the ballot): 153 -> 142 us on the 128 x 1000
+// microbenchmark but no change in the bench (0.99 vs 1.00 ms per step), and a guard against exp2
+// overflow (re-run on a non-finite row sum) spilled 18 VGPRs (1.6 ms): dropped.
 // ------------------------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VAP_DEV f32x16 mfma32(chunk16 a, chunk16 b, f32x16 c) {
@@ -390,204 +394,6 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
   }
 }
 
-__global__ __launch_bounds__(256, 3) void attn6_kernel(AttnArgs a, int nqb, int grp) {
-  __shared__ __attribute__((aligned(16))) unsigned char kv[2][2][KB2 * TROW];  // [buf][K,V]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int npair = a.H * a.S;
-  int hs, qb;
-  if (grp > 0 && (npair & 7) == 0) {
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, px = npair >> 3;  // pairs per XCD
-    const int g = j / (grp * nqb), r = j - g * grp * nqb;
-    const int gp = min(grp, px - g * grp);                                // pairs in this group
-    const int lv = r / gp;
-    qb = nqb - 1 - lv;
-    hs = (g * grp + (r - lv * gp)) * 8 + x;
-  } else {
-    hs = blockIdx.x % npair;
-    qb = nqb - 1 - (int)(blockIdx.x / npair);
-  }
-  const int h = hs % a.H, s = hs / a.H;
-  const int ks = a.kv_swap ? (s ^ 1) : s;
-  const bf16* Qs = (const bf16*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
-  const __amdgpu_buffer_rsrc_t rK = make_rsrc((const bf16*)a.K + (int64_t)ks * a.k_seq + h * HDIM, (uint32_t)a.T * a.k_ld * 2);
-  const __amdgpu_buffer_rsrc_t rV = make_rsrc((const bf16*)a.V + (int64_t)ks * a.v_seq + h * HDIM, (uint32_t)a.T * a.v_ld * 2);
-  constexpr float LOG2E = 1.4426950408889634f;
-  constexpr float TAU = 8.0f;
-  const float c2 = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
-  const int qw0 = a.q0 + qb * QB2 + w * 32;  // first query of this wave
-  const int qlast = min(a.q0 + qb * QB2 + QB2 - 1, a.T - 1);
-  const int nkb = qlast / KB2 + 1;
-  const int hl = lane >> 5, ql = lane & 31;
-  const int qv = qw0 + ql;  // this lane's query
-
-  // Q'^T fragments (B of the S MFMA): lane holds dims 16k + 8h .. +8 of its query, pre-scaled
-  chunk16 qf[4];
-  {
-    const int qc = qv < a.T ? qv : a.T - 1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bf16x8 q = *(const bf16x8*)(Qs + (int64_t)qc * a.q_ld + 16 * k + 8 * hl);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = (bf16)((float)q[e] * c2);
-      qf[k] = __builtin_bit_cast(chunk16, q);
-    }
-  }
-  // key bias of the lane's S registers within a 32-key tile (the C operand of the S MFMA)
-  f32x16 kb0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) kb0[r] = sl2 * (float)(8 * (r >> 2) + 4 * hl + (r & 3));
-  const float off32 = sl2 * 32.0f, off64 = sl2 * (float)KB2;
-
-  float m = -INFINITY;  // running max of the true log2 scores
-  f32x16 o0 = {}, o1 = {}, ls = {};
-  const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
-  const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
-
-  // staging: 2 K + 2 V chunks per thread, scalar tile offset
-  const int srow = tid >> 3, sc = tid & 7;
-  const uint32_t vkoff0 = (uint32_t)(srow * a.k_ld + sc * 8) * 2, vkoff1 = vkoff0 + 32u * a.k_ld * 2;
-  const uint32_t vvoff0 = (uint32_t)(srow * a.v_ld + sc * 8) * 2, vvoff1 = vvoff0 + 32u * a.v_ld * 2;
-  const uint32_t ktile = (uint32_t)KB2 * a.k_ld * 2, vtile = (uint32_t)KB2 * a.v_ld * 2;
-  const int ldsK0 = srow * TROW + kswz2(srow, sc) * 16, ldsK1 = (srow + 32) * TROW + kswz2(srow + 32, sc) * 16;
-  const int ldsV0 = srow * TROW + vswz4(srow, sc) * 16, ldsV1 = (srow + 32) * TROW + vswz4(srow + 32, sc) * 16;
-  chunk16 rk[2], rv[2];
-  auto gload = [&](int kb) {
-    rk[0] = buf_load16(rK, vkoff0, kb * ktile);
-    rk[1] = buf_load16(rK, vkoff1, kb * ktile);
-    rv[0] = buf_load16(rV, vvoff0, kb * vtile);
-    rv[1] = buf_load16(rV, vvoff1, kb * vtile);
-  };
-  auto lstore = [&](int buf) {
-    *(chunk16*)(kv[buf][0] + ldsK0) = rk[0];
-    *(chunk16*)(kv[buf][0] + ldsK1) = rk[1];
-    *(chunk16*)(kv[buf][1] + ldsV0) = rv[0];
-    *(chunk16*)(kv[buf][1] + ldsV1) = rv[1];
-  };
-  // K fragment of key tile t, k-step k: row 32t + ql, chunk 2k + hl (the 32t part is an immediate)
-  int koff[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) koff[k] = ql * TROW + kswz2(ql, 2 * k + hl) * 16;
-  // V^T fragment, dims 32u + ql, keys 32t + 16s + 4hl + {0..3} (+8 for elements 4..7): the lane
-  // supplies row 4hl + q, columns 32u + 16(g&1) + 4p of its 16-lane group g (lane = 16g + 4q + p)
-  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
-  int voff[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    voff[u] = (4 * hl + tq) * TROW + vswz4(4 * hl + tq, 4 * u + 2 * tg + (tp >> 1)) * 16 + (tp & 1) * 8;
-
-  // key tiles from the diagonal DOWN (kb = nkb-1 .. 0): the wave's top two visible tiles hold every
-  // query's diagonal and the largest AliBi key bias, so they set the running max; the older tiles
-  // skip the tile max (15 v_max3 + a permlane + the ballot per tile) and take exp2(s - m) as is.
-  // A score far above that max could overflow exp2 (s - m > 127): any non-finite row sum at the end
-  // re-runs the workgroup's tiles with the max on every tile (`safe`), so no input can break it.
-  const int top = (qw0 + 31) / KB2;  // the wave's highest visible tile
-  bool safe = false;
-  auto tile = [&](int kb, auto cur_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    if (kb > 0) gload(kb - 1);
-    const int key0 = kb * KB2;
-    if (key0 <= qw0 + 31) {  // wave-uniform: some key of the tile is visible to some query of the wave
-      const unsigned char* Kt = kv[cur][0];
-      const unsigned char* Vt = kv[cur][1];
-      f32x16 st[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        st[t] = kb0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st[t] = mfma32(*(const chunk16*)(Kt + t * 32 * TROW + koff[k]), qf[k], st[t]);
-      }
-      if (key0 + KB2 - 1 > qw0) {  // wave-uniform: a diagonal tile
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (key0 + 32 * t + 8 * (r >> 2) + 4 * hl + (r & 3) > qv) st[t][r] = -INFINITY;
-      }
-      const float tofs = off64 * (float)kb;
-      if (safe || kb >= top - 1) {  // wave-uniform
-        float b0 = st[0][0], b1 = st[1][0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) {
-          b0 = fmaxf(b0, st[0][r]);
-          b1 = fmaxf(b1, st[1][r]);
-        }
-        const float bm = xmax2(fmaxf(b0, b1 + off32)) + tofs;  // the tile's max true score of the lane's query
-        if (__ballot(bm > m + TAU)) {  // wave-uniform: raise the running max, rescale O and the sums
-          const float mn = fmaxf(m, bm);
-          const float alpha = __builtin_amdgcn_exp2f(m - mn);
-          m = mn;
-          o0 *= alpha;
-          o1 *= alpha;
-          ls *= alpha;
-        }
-      }
-      const float m0 = m - tofs, m1 = m0 - off32;
-      bf16x8 pb[2][2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const float mt = t ? m1 : m0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) pb[t][k][e] = (bf16)__builtin_amdgcn_exp2f(st[t][8 * k + e] - mt);
-        }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const chunk16 p = __builtin_bit_cast(chunk16, pb[t][k]);
-          const int ro = (32 * t + 16 * k) * TROW;
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const u32x2 v0 = tr_read(Vt + ro + voff[u]);
-            const u32x2 v1 = tr_read(Vt + ro + 8 * TROW + voff[u]);
-            const chunk16 vf = {v0.x, v0.y, v1.x, v1.y};
-            if (u == 0) o0 = mfma32(vf, p, o0);
-            else o1 = mfma32(vf, p, o1);
-          }
-          ls = mfma32(ones, p, ls);
-        }
-    }
-    if (kb > 0) lstore(cur ^ 1);
-    __syncthreads();
-  };
-
-  __shared__ int redo;
-  for (int pass = 0; pass < 2; ++pass) {
-    gload(nkb - 1);
-    lstore(0);
-    if (tid == 0) redo = 0;
-    __syncthreads();
-    for (int i = 0; i < nkb; i += 2) {  // unrolled by 2: the LDS buffer index is a constant
-      tile(nkb - 1 - i, std::integral_constant<int, 0>{});
-      if (i + 1 < nkb) tile(nkb - 2 - i, std::integral_constant<int, 1>{});
-    }
-#if VAP_ATTN_NOGUARD
-    break;
-#endif
-    if (pass == 1) break;
-    // a non-finite row sum (only from a skipped tile max): the whole workgroup runs again with the max
-    if (__ballot(!__builtin_isfinite(ls[0])) && lane == 0) redo = 1;
-    __syncthreads();
-    if (!redo) break;
-    safe = true;
-    m = -INFINITY;
-    o0 = f32x16{};
-    o1 = f32x16{};
-    ls = f32x16{};
-  }
-  // O^T: lane holds its query's dims 32u + 8g + 4hl + e in register 4g + e of o_u
-  const float inv = 1.0f / ls[0];
-  if (qv < a.T) {
-    bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv * a.o_ld + h * HDIM;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      store4(orow + 8 * g + 4 * hl, o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-      store4(orow + 32 + 8 * g + 4 * hl, o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-    }
-  }
-}
-
 }  // namespace
 
 template <typename T>
@@ -597,11 +403,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
     if (a.q0 < 0 || a.q0 >= a.T) return hipErrorInvalidValue;
     const int nqb = (a.T - a.q0 + QB2 - 1) / QB2;
     constexpr int grp = 8;  // (sequence, head) pairs per XCD group: K/V of 8 pairs x <= 256 KiB in L2
-#if VAP_ATTN_REV
-    hipLaunchKernelGGL(attn6_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
-#else
     hipLaunchKernelGGL(attn4_kernel, dim3(nqb * a.H * a.S), dim3(256), 0, st, a, nqb, grp);
-#endif
     return hipGetLastError();
   }
   if (a.q0 != 0) return hipErrorInvalidValue;
