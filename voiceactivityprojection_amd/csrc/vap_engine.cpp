@@ -1263,6 +1263,7 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
     HIPCHK(hipEventRecord(fk, st));
     HIPCHK(hipStreamWaitEvent(h->side[2], fk, 0));
   }
+  // (the second group on side[2] at normal priority, after the front end's end, measured -2.5 %)
   int rc;
   for (int k = 0; k < t.nbe; ++k) {
     const int c = t.be_end[k] - 1;  // the last recurrence chunk of back-end chunk k
