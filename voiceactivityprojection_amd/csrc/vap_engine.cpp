@@ -63,6 +63,7 @@ struct vap_handle {
   // pieces 0.1 / 0.27 / 0.48 / 0.72 in a same-box A/B: a smaller last piece shortens what the recurrence
   // still has to do after the front end's end)
   std::vector<double> tc_fe{0.12, 0.3, 0.5, 0.7, 0.85}, tc_be{0.64};
+  bool tc_be_auto = true;  // back-end chunks of clips longer than 1200 frames by rule (tc_schedule_split)
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
@@ -1144,7 +1145,23 @@ TcSched tc_schedule_split(const vap_handle* h, const Plan& p) {
   if (h->tc_fe.empty() || h->tc_be.empty() || T_ < 128) return tc_schedule(h, p);
   std::vector<std::tuple<int, bool, bool>> bd;  // frame, front-end boundary, back-end boundary
   for (double f : h->tc_fe) bd.emplace_back((int)(T_ * f + 0.5), true, false);
-  for (double f : h->tc_be) bd.emplace_back((int)(T_ * f + 0.5), false, true);
+  if (h->tc_be_auto && T_ > 1200) {
+    // long clips (the recurrence binds: 2 T dependent steps): chunks shrinking toward the end, so each
+    // one's back end runs in the shadow of the recurrence's next chunk and the part after the
+    // recurrence's end keeps its 20 s size: from the end ~360, 540, 810, ... frames (x1.5), the rest
+    // one chunk, boundaries on 128 frames (whole attention q-blocks).  32 x 60 s: [1280, 2048, 2560];
+    // 129.8k audio-s/s with the 20 s fraction 0.64, 142.2-143.6k with 0.4 / 0.7 / 0.88
+    double sz = 360, pos = T_;
+    int prev = T_;
+    while ((pos -= sz) >= 384) {
+      const int b = (int)pos / 128 * 128;
+      if (b < prev) bd.emplace_back(b, false, true);
+      prev = b;
+      sz *= 1.5;
+    }
+  } else {
+    for (double f : h->tc_be) bd.emplace_back((int)(T_ * f + 0.5), false, true);
+  }
   std::sort(bd.begin(), bd.end());
   std::vector<std::tuple<int, bool, bool>> m;  // merged: boundaries closer than 24 frames become one
   for (auto& b : bd) {
@@ -1884,7 +1901,10 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
     }
   };
   if (const char* e = getenv("VAP_TC_FE")) parse_list(e, h->tc_fe);
-  if (const char* e = getenv("VAP_TC_BE")) parse_list(e, h->tc_be);
+  if (const char* e = getenv("VAP_TC_BE")) {
+    parse_list(e, h->tc_be);
+    h->tc_be_auto = false;
+  }
 
   if (h->time_chunks > vap_handle::MAXMB) h->time_chunks = vap_handle::MAXMB;
   if (h->microbatches > vap_handle::MAXMB) h->microbatches = vap_handle::MAXMB;
