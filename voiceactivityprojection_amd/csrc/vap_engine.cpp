@@ -63,7 +63,8 @@ struct vap_handle {
   // pieces 0.1 / 0.27 / 0.48 / 0.72 in a same-box A/B: a smaller last piece shortens what the recurrence
   // still has to do after the front end's end)
   std::vector<double> tc_fe{0.12, 0.3, 0.5, 0.7, 0.85}, tc_be{0.64};
-  bool tc_be_auto = true;  // back-end chunks of clips longer than 1200 frames by rule (tc_schedule_split)
+  bool tc_be_auto = true;
+  bool tc_fe_auto = true;  // + a 120-frame first front-end piece for clips longer than 1200 frames  // back-end chunks of clips longer than 1200 frames by rule (tc_schedule_split)
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
@@ -1145,6 +1146,9 @@ TcSched tc_schedule_split(const vap_handle* h, const Plan& p) {
   if (h->tc_fe.empty() || h->tc_be.empty() || T_ < 128) return tc_schedule(h, p);
   std::vector<std::tuple<int, bool, bool>> bd;  // frame, front-end boundary, back-end boundary
   for (double f : h->tc_fe) bd.emplace_back((int)(T_ * f + 0.5), true, false);
+  // long clips: a first front-end piece of the 20 s clip's first-piece size (120 frames), so the
+  // recurrence starts as early as at 20 s (32 x 60 s: +1.5 %)
+  if (h->tc_fe_auto && T_ > 1200) bd.emplace_back(120, true, false);
   if (h->tc_be_auto && T_ > 1200) {
     // long clips (the recurrence binds: 2 T dependent steps): chunks shrinking toward the end, so each
     // one's back end runs in the shadow of the recurrence's next chunk and the part after the
@@ -1900,7 +1904,10 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
       a = b + 1;
     }
   };
-  if (const char* e = getenv("VAP_TC_FE")) parse_list(e, h->tc_fe);
+  if (const char* e = getenv("VAP_TC_FE")) {
+    parse_list(e, h->tc_fe);
+    h->tc_fe_auto = false;
+  }
   if (const char* e = getenv("VAP_TC_BE")) {
     parse_list(e, h->tc_be);
     h->tc_be_auto = false;
