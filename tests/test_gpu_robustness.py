@@ -231,3 +231,17 @@ def test_back_end_split_bit_identical(monkeypatch):
         m.synchronize()
         for k in ref:
             assert torch.equal(out[k], ref[k]), (split, frac, k)
+
+
+def test_long_clip_schedule_bit_identical(monkeypatch):
+    """Clips longer than 1200 frames get their own time chunking (an extra 120-frame first front-end
+    piece, back-end chunks shrinking toward the end); the outputs do not depend on the chunking."""
+    w = _batch(2, 960000, 77)  # 60 s: T = 3000
+    ref = _model().probs(w)  # automatic long-clip chunks
+    monkeypatch.setenv("VAP_TC_BE", "0.64")
+    monkeypatch.setenv("VAP_TC_FE", "0.1,0.27,0.48,0.72")
+    m = _model()
+    out = m.probs(w)
+    m.synchronize()
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
