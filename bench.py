@@ -61,8 +61,10 @@ def class_flops(B: int, n: int, heads: int = 4, channel_layers: int = 1, cross_l
     return f, L
 
 
-def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int = 32):
-    """Time the CPU oracle (torch fp32 restatement of the reference) on a bounded sample."""
+def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int = 32, batch: int = 4):
+    """Time the CPU oracle (torch fp32 restatement of the reference) on a bounded sample: batches of
+    `batch` clips of the workload's length (the GPU workload's shape, fewer clips per call) until the
+    budget is spent."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import vap_oracle as O
     from voiceactivityprojection_amd.weights import synthetic_waveform
@@ -72,16 +74,19 @@ def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int =
     sd = O.state_dict_to_torch(sd_np)
     n = int(seconds * 16000)
     O.probs(torch.from_numpy(synthetic_waveform(0, 16000 * 3)[None]), sd)  # warm-up
-    done, t0 = 0, time.perf_counter()
+    done, calls, t0 = 0, 0, time.perf_counter()
     while done < max_clips:
-        O.probs(torch.from_numpy(synthetic_waveform(done, n)[None]), sd)
-        done += 1
+        w = np.stack([synthetic_waveform(done + i, n) for i in range(batch)])
+        O.probs(torch.from_numpy(w), sd)
+        done += batch
+        calls += 1
         if time.perf_counter() - t0 > budget_s:
             break
     el = time.perf_counter() - t0
     return {"value": round(done * seconds / el, 3), "unit": "audio-s/s", "cores": threads, "kind": "port",
-            "sample": f"{done} x {seconds:g} s stereo clip(s), batch 1, oracle/vap_oracle.py fp32 on "
-                      f"{threads} host threads ({el:.1f} s)"}
+            "nproc": os.cpu_count(),
+            "sample": f"{calls} call(s) of {batch} x {seconds:g} s stereo clips, oracle/vap_oracle.py fp32 on "
+                      f"{threads} host threads ({el:.1f} s; nproc {os.cpu_count()})"}
 
 
 def parse_args(argv=None):
