@@ -27,7 +27,7 @@ def main():
     model.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed=0).items()}, strict=True)
     model = model.to(dev).eval()
     wav = torch.from_numpy(synthetic_batch(0, 64, 320000)).to(dev)
-    for _ in range(3):
+    for _ in range(int(os.environ.get("REPS", "3"))):
         model.probs(wav)
     torch.cuda.synchronize()
     buf = np.zeros((8, 24), dtype=np.uint64)
@@ -37,7 +37,8 @@ def main():
     for i in range(8):
         st = buf[i].astype(np.int64)
         d = np.diff(st[:n])
-        print(f"wg{i}: total {st[n - 1] - st[0]:7d} | " + " ".join(f"{k}={v}" for k, v in zip(names, d)))
+        ghz = (st[n - 1] - st[0]) / max(1, st[23] - st[22]) * 0.1
+        print(f"wg{i}: total {st[n - 1] - st[0]:7d} | " + " ".join(f"{k}={v}" for k, v in zip(names, d)) + f" | clock {ghz:.2f} GHz")
 
 
 if __name__ == "__main__":

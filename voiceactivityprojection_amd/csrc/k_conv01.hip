@@ -127,8 +127,9 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   const int s = blockIdx.y;
   const int t0 = r0 + blockIdx.x * BM2;
   const int samp = (STAMPS && (blockIdx.x == 0 || blockIdx.x == 3) && s < 4) ? (s * 2 + (blockIdx.x == 3)) : -1;
-  unsigned long long stv[10];
+  unsigned long long stv[10], rt0 = 0;
   int nst = 0;
+  if constexpr (STAMPS) rt0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the clock held = d(memtime) / d(rt)
   auto stamp = [&]() {
     if constexpr (STAMPS) {
       __builtin_amdgcn_sched_barrier(0);
@@ -414,8 +415,12 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   if constexpr (STAMPS) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp();
-    if (samp >= 0 && tid == 0)
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+    if (samp >= 0 && tid == 0) {
       for (int k = 0; k < 10 && k < nst; ++k) g_conv01_stamps[samp][k] = stv[k];
+      g_conv01_stamps[samp][22] = rt0;
+      g_conv01_stamps[samp][23] = rt1;
+    }
   }
 }
 

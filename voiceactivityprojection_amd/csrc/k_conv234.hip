@@ -38,8 +38,8 @@ constexpr int CK_HALF = CK_HR * 64;        // 17408 B
 constexpr int CK_SLAB = 2 * CK_HALF;       // 34816 B
 constexpr int CK_RED = 3 * CK_SLAB;        // 104448: [256 rows][8 waves] (mean, M2) float2 (epilogue)
 constexpr int CK_PAR = CK_RED + 256 * 8 * 8;  // 120832: bias | gamma | beta, 3 x 256 fp32
-constexpr int CK_ST = CK_PAR + 3 * 256 * 4;   // 123904: 12 phase stamps (VAP_CONVK4_DBG=16)
-constexpr int CK_LDS = CK_ST + 12 * 8;        // 124000 B
+constexpr int CK_ST = CK_PAR + 3 * 256 * 4;   // 123904: 12 phase stamps + 2 real-time stamps (VAP_CONVK4_DBG=16)
+constexpr int CK_LDS = CK_ST + 14 * 8;        // 124016 B
 constexpr int CK_PIECES = 2 * (CK_HR / 16);  // 34 DMA pieces of 16 half-rows x 64 B per slab
 
 VAP_DEV int ck_phys(int row, int c) { return (c + (row >> 2)) & 3; }
@@ -93,7 +93,18 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  // (DBG 16) the 100 MHz real-time counter beside the first and last shader-clock stamps: the
+  // clock the chip holds under this kernel = d(memtime) / d(memrealtime) x 100 MHz
+  auto rstamp = [&](int k) {
+    if constexpr ((DBG & 16) != 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long v = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) ((unsigned long long*)(smem + CK_ST))[12 + k] = v;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   stamp();
+  rstamp(0);
   if (tid < 192) {  // bias | gamma | beta -> LDS
     const float* src = tid < 64 ? a.bias : (tid < 128 ? a.gamma : a.beta);
     ((f32x4*)(smem + CK_PAR))[tid] = ((const f32x4*)src)[tid & 63];
@@ -369,8 +380,9 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
         stamp();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp();
+        rstamp(1);
         if (s == 0 && t0 < 8 * 256 && tid == 0)
-          for (int k = 0; k < 12; ++k) a.stamps[(t0 >> 8) * 12 + k] = ((const unsigned long long*)(smem + CK_ST))[k];
+          for (int k = 0; k < 14; ++k) a.stamps[(t0 >> 8) * 14 + k] = ((const unsigned long long*)(smem + CK_ST))[k];
       }
     }
     if (!has_next) break;

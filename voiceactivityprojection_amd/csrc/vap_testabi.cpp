@@ -77,12 +77,12 @@ int vap_test_convk4(const void* in, int64_t in_seq, int in_rows, const void* W, 
   if (hipMalloc(&wks, 256 * 1024 * 2) != hipSuccess) return VAP_ERR_HIP;
   int rc = rc_of(launch_pack_kstep((const bf16*)W, (bf16*)wks, 256, 1024, st));
   static unsigned long long* stamps = nullptr;
-  if (dbg & 16 && !stamps && hipMalloc(&stamps, 8 * 12 * 8) != hipSuccess) return VAP_ERR_HIP;
+  if (dbg & 16 && !stamps && hipMalloc(&stamps, 8 * 14 * 8) != hipSuccess) return VAP_ERR_HIP;
   ConvK4Args a{(const bf16*)in, in_seq, in_rows, (const bf16*)wks, bias, gamma, beta, (bf16*)out, out_seq, M, dbg, stamps};
   if (rc == VAP_OK) rc = rc_of(launch_convk4(a, S, st));
   if (hipStreamSynchronize(st) != hipSuccess) rc = VAP_ERR_HIP;
   (void)hipFree(wks);
-  if (dbg & 16 && stamps_out && hipMemcpy(stamps_out, stamps, 8 * 12 * 8, hipMemcpyDeviceToHost) != hipSuccess) rc = VAP_ERR_HIP;
+  if (dbg & 16 && stamps_out && hipMemcpy(stamps_out, stamps, 8 * 14 * 8, hipMemcpyDeviceToHost) != hipSuccess) rc = VAP_ERR_HIP;
   return rc;
 }
 
