@@ -171,44 +171,74 @@ __global__ __launch_bounds__(256) void convert_rows_kernel(const float* __restri
 // probs() epilogue (model.py:189-213): softmax, sigmoid VAD, entropy H = sum -p log2 p, and
 // probs_next_speaker_aggregate (objective.py:184-204) for the now / future bin ranges:
 //   abp[k, c] = popcount(bits of k in [c*nb+from, c*nb+to]);  p = probs . abp;  p /= sum_c p + 1e-5
-// One wave per frame, 4 classes per lane (n_classes = 256).
+// One 16-lane row per frame (4 frames per wave), 16 classes per lane: lane l holds classes
+// 64k + 4l .. +3 (k = 0..3), so each of the four 16-B loads of a row reads 256 contiguous bytes,
+// and every reduction is 4 DPP steps inside the row (a wave per frame took 6 steps per reduction
+// for 4 classes per lane, and one 16-B load per lane: 45 us per bench epilogue).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
-                                                   int64_t frames, int nb, int now0, int now1, int fut0, int fut1,
-                                                   float* __restrict__ probs, float* __restrict__ vad,
-                                                   float* __restrict__ p_now, float* __restrict__ p_future,
-                                                   float* __restrict__ H) {
-  const int lane = threadIdx.x & 63;
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= frames) return;
-  const f32x4 x = *(const f32x4*)(logits + f * 256 + lane * 4);
-  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
-  f32x4 e;
+VAP_DEV float row_sum16(float v) {  // sum over the lane's 16-lane row; every lane gets the same bits
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+VAP_DEV float row_max16(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+// Softmax pieces of one frame's 256 logits `lg` held by a 16-lane row: e = exp(x - max), its sum.
+// Shared by probs_kernel, labels_loss_kernel and probs_loss_kernel, so their outputs are bit-identical.
+VAP_DEV void soft16(const float* __restrict__ lg, int l16, f32x4 (&e)[4], float& mx, float& sum) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
-  const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
-  const f32x4 p = e * (1.0f / sum);  // one IEEE division per lane (four were VALU-bound)
-  *(f32x4*)(probs + f * 256 + lane * 4) = p;
-  float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
+  for (int k = 0; k < 4; ++k) e[k] = *(const f32x4*)(lg + 64 * k + 4 * l16);
+  float m = e[0][0];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m = fmaxf(m, e[k][i]);
+  mx = row_max16(m);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[k][i] = expf(e[k][i] - mx);
+    s += (e[k][0] + e[k][1]) + (e[k][2] + e[k][3]);
+  }
+  sum = row_sum16(s);
+}
+// probs, H, p_now / p_future of one frame from soft16's pieces (lane l16 of the frame's row);
+// the row's lane 0 writes the per-frame scalars and the VAD sigmoid.
+VAP_DEV void probs_frame(int64_t f, int l16, f32x4 (&e)[4], float sum, int nb, int now0, int now1, int fut0,
+                         int fut1, const float* __restrict__ vadl, float* __restrict__ probs, float* __restrict__ vad,
+                         float* __restrict__ p_now, float* __restrict__ p_future, float* __restrict__ H) {
+  const float inv = 1.0f / sum;  // one IEEE division per lane (one per class was VALU-bound)
   const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
   const unsigned mfut = ((1u << (fut1 - fut0 + 1)) - 1u) << fut0;
   const unsigned bm = (1u << nb) - 1u;
+  float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const unsigned k = lane * 4 + i;
-    h += -p[i] * log2f(p[i]);
-    const unsigned k0 = k & bm, k1 = (k >> nb) & bm;
-    n0 += p[i] * (float)__popc(k0 & mnow);
-    n1 += p[i] * (float)__popc(k1 & mnow);
-    u0 += p[i] * (float)__popc(k0 & mfut);
-    u1 += p[i] * (float)__popc(k1 & mfut);
+  for (int k = 0; k < 4; ++k) {
+    const f32x4 p = e[k] * inv;
+    *(f32x4*)(probs + f * 256 + 64 * k + 4 * l16) = p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned c = 64 * k + 4 * l16 + i;
+      h += -p[i] * log2f(p[i]);
+      const unsigned k0 = c & bm, k1 = (c >> nb) & bm;
+      n0 += p[i] * (float)__popc(k0 & mnow);
+      n1 += p[i] * (float)__popc(k1 & mnow);
+      u0 += p[i] * (float)__popc(k0 & mfut);
+      u1 += p[i] * (float)__popc(k1 & mfut);
+    }
   }
-  h = wave_sum(h);
-  n0 = wave_sum(n0);
-  n1 = wave_sum(n1);
-  u0 = wave_sum(u0);
-  u1 = wave_sum(u1);
-  if (lane == 0) {
+  h = row_sum16(h);
+  n0 = row_sum16(n0);
+  n1 = row_sum16(n1);
+  u0 = row_sum16(u0);
+  u1 = row_sum16(u1);
+  if (l16 == 0) {
     H[f] = h;
     const float dn = n0 + n1 + 1e-5f, du = u0 + u1 + 1e-5f;
     p_now[f * 2 + 0] = n0 / dn;
@@ -220,6 +250,20 @@ __global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ lo
   }
 }
 
+__global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
+                                                   int64_t frames, int nb, int now0, int now1, int fut0, int fut1,
+                                                   float* __restrict__ probs, float* __restrict__ vad,
+                                                   float* __restrict__ p_now, float* __restrict__ p_future,
+                                                   float* __restrict__ H) {
+  const int l16 = threadIdx.x & 15;
+  const int64_t f = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (f >= frames) return;  // row-uniform: the DPP reductions stay inside fully active rows
+  f32x4 e[4];
+  float mx, sum;
+  soft16(logits + f * 256, l16, e, mx, sum);
+  probs_frame(f, l16, e, sum, nb, now0, now1, fut0, fut1, vadl, probs, vad, p_now, p_future, H);
+}
+
 // ------------------------------------------------------------------------------------------
 // get_labels (objective.py:40-76,112-139; integer bit packing, bit-exact for binary VA) and
 // loss_vap(reduction='none') (objective.py:220-243) for frames t < T - horizon.
@@ -228,14 +272,14 @@ __global__ __launch_bounds__(256) void probs_kernel(const float* __restrict__ lo
 __global__ __launch_bounds__(256) void labels_loss_kernel(const float* __restrict__ logits, const float* __restrict__ va,
                                                          int B, int Tn, int nl, int4 bf, int nb, float thr,
                                                          int64_t* __restrict__ labels, float* __restrict__ loss) {
-  const int lane = threadIdx.x & 63;
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B * nl
+  const int l16 = threadIdx.x & 15, row = (threadIdx.x & 63) >> 4;
+  const int64_t f = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // over B * nl, one 16-lane row each
   if (f >= (int64_t)B * nl) return;
   const int b = (int)(f / nl), t = (int)(f - (int64_t)b * nl);
   const int bfr[4] = {bf.x, bf.y, bf.z, bf.w};
   bool bit = false;
-  if (lane < 2 * nb) {
-    const int c = lane / nb, bin = lane - c * nb;
+  if (l16 < 2 * nb) {
+    const int c = l16 / nb, bin = l16 - c * nb;
     int start = 0;
     for (int i = 0; i < bin; ++i) start += bfr[i];
     const float* p = va + ((int64_t)b * Tn + t + 1 + start) * 2 + c;
@@ -244,17 +288,17 @@ __global__ __launch_bounds__(256) void labels_loss_kernel(const float* __restric
     bit = (s / (float)bfr[bin]) >= thr;
   }
   const unsigned long long m = __ballot(bit);
-  // bit index of lane j = c*nb + bin == lane
-  const int64_t label = (int64_t)(m & ((1ull << (2 * nb)) - 1ull));
+  // bit index of row lane j = c*nb + bin == j
+  const int64_t label = (int64_t)((m >> (16 * row)) & ((1ull << (2 * nb)) - 1ull));
   if (!logits) {
-    if (lane == 0) labels[f] = label;
+    if (l16 == 0) labels[f] = label;
     return;
   }
   const float* lg = logits + ((int64_t)b * Tn + t) * 256;
-  const f32x4 x = *(const f32x4*)(lg + lane * 4);
-  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
-  const float se = wave_sum(expf(x[0] - mx) + expf(x[1] - mx) + expf(x[2] - mx) + expf(x[3] - mx));
-  if (lane == 0) {
+  f32x4 e[4];
+  float mx, se;
+  soft16(lg, l16, e, mx, se);
+  if (l16 == 0) {
     labels[f] = label;
     loss[f] = (mx + logf(se)) - lg[label];
   }
@@ -303,45 +347,14 @@ __global__ __launch_bounds__(256) void probs_loss_kernel(const float* __restrict
                                                         float* __restrict__ p_now, float* __restrict__ p_future,
                                                         float* __restrict__ H, const int64_t* __restrict__ labels,
                                                         int nl, float* __restrict__ loss) {
-  const int lane = threadIdx.x & 63;
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l16 = threadIdx.x & 15;
+  const int64_t f = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   if (f >= frames) return;
-  const f32x4 x = *(const f32x4*)(logits + f * 256 + lane * 4);
-  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
-  f32x4 e;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = expf(x[i] - mx);
-  const float sum = wave_sum(e[0] + e[1] + e[2] + e[3]);
-  const f32x4 p = e * (1.0f / sum);  // one IEEE division per lane (four were VALU-bound)
-  *(f32x4*)(probs + f * 256 + lane * 4) = p;
-  float h = 0.f, n0 = 0.f, n1 = 0.f, u0 = 0.f, u1 = 0.f;
-  const unsigned mnow = ((1u << (now1 - now0 + 1)) - 1u) << now0;
-  const unsigned mfut = ((1u << (fut1 - fut0 + 1)) - 1u) << fut0;
-  const unsigned bm = (1u << nb) - 1u;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const unsigned k = lane * 4 + i;
-    h += -p[i] * log2f(p[i]);
-    const unsigned k0 = k & bm, k1 = (k >> nb) & bm;
-    n0 += p[i] * (float)__popc(k0 & mnow);
-    n1 += p[i] * (float)__popc(k1 & mnow);
-    u0 += p[i] * (float)__popc(k0 & mfut);
-    u1 += p[i] * (float)__popc(k1 & mfut);
-  }
-  h = wave_sum(h);
-  n0 = wave_sum(n0);
-  n1 = wave_sum(n1);
-  u0 = wave_sum(u0);
-  u1 = wave_sum(u1);
-  if (lane == 0) {
-    H[f] = h;
-    const float dn = n0 + n1 + 1e-5f, du = u0 + u1 + 1e-5f;
-    p_now[f * 2 + 0] = n0 / dn;
-    p_now[f * 2 + 1] = n1 / dn;
-    p_future[f * 2 + 0] = u0 / du;
-    p_future[f * 2 + 1] = u1 / du;
-    vad[f * 2 + 0] = 1.0f / (1.0f + expf(-vadl[f * 2 + 0]));
-    vad[f * 2 + 1] = 1.0f / (1.0f + expf(-vadl[f * 2 + 1]));
+  f32x4 e[4];
+  float mx, sum;
+  soft16(logits + f * 256, l16, e, mx, sum);
+  probs_frame(f, l16, e, sum, nb, now0, now1, fut0, fut1, vadl, probs, vad, p_now, p_future, H);
+  if (l16 == 0) {
     const int64_t b = f / Tn;
     const int t = (int)(f - b * Tn);
     if (t < nl) {
@@ -494,7 +507,7 @@ hipError_t launch_probs(const float* logits, const float* vad_logits, int B, int
                         int fut0, int fut1, float* probs, float* vad, float* p_now, float* p_future, float* H,
                         hipStream_t st) {
   const int64_t frames = (int64_t)B * Tn;
-  hipLaunchKernelGGL(probs_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, logits, vad_logits, frames,
+  hipLaunchKernelGGL(probs_kernel, dim3((unsigned)((frames + 15) / 16)), dim3(256), 0, st, logits, vad_logits, frames,
                      n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H);
   return hipGetLastError();
 }
@@ -512,7 +525,7 @@ hipError_t launch_labels_loss(const float* logits, const float* va, int B, int T
   const int nl = Tn - horizon;
   if (nl <= 0) return hipErrorInvalidValue;
   const int64_t n = (int64_t)B * nl;
-  hipLaunchKernelGGL(labels_loss_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, logits, va, B, Tn, nl, bf,
+  hipLaunchKernelGGL(labels_loss_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, logits, va, B, Tn, nl, bf,
                      n_bins, threshold, labels, loss);
   return hipGetLastError();
 }
@@ -534,7 +547,7 @@ hipError_t launch_probs_loss(const float* logits, const float* vad_logits, int B
   hipLaunchKernelGGL(labels_lds_kernel, dim3((unsigned)((nl + LB_T - 1) / LB_T), (unsigned)B), dim3(LB_T), 0, st,
                      vad_logits, Tn, nl, bf, n_bins, threshold, labels);
   const int64_t frames = (int64_t)B * Tn;
-  hipLaunchKernelGGL(probs_loss_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, logits, vad_logits, Tn,
+  hipLaunchKernelGGL(probs_loss_kernel, dim3((unsigned)((frames + 15) / 16)), dim3(256), 0, st, logits, vad_logits, Tn,
                      frames, n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H, labels, nl, loss);
   return hipGetLastError();
 }
