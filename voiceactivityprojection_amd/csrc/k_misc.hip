@@ -190,9 +190,11 @@ VAP_DEV float row_max16(float v) {
 }
 // Softmax pieces of one frame's 256 logits `lg` held by a 16-lane row: e = exp(x - max), its sum.
 // Shared by probs_kernel, labels_loss_kernel and probs_loss_kernel, so their outputs are bit-identical.
-VAP_DEV void soft16(const float* __restrict__ lg, int l16, f32x4 (&e)[4], float& mx, float& sum) {
+VAP_DEV void soft16_load(const float* __restrict__ lg, int l16, f32x4 (&e)[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) e[k] = *(const f32x4*)(lg + 64 * k + 4 * l16);
+}
+VAP_DEV void soft16_exp(f32x4 (&e)[4], float& mx, float& sum) {  // logits in e -> exp(x - max) in e
   float m = e[0][0];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -207,6 +209,10 @@ VAP_DEV void soft16(const float* __restrict__ lg, int l16, f32x4 (&e)[4], float&
     s += (e[k][0] + e[k][1]) + (e[k][2] + e[k][3]);
   }
   sum = row_sum16(s);
+}
+VAP_DEV void soft16(const float* __restrict__ lg, int l16, f32x4 (&e)[4], float& mx, float& sum) {
+  soft16_load(lg, l16, e);
+  soft16_exp(e, mx, sum);
 }
 // probs, H, p_now / p_future of one frame from soft16's pieces (lane l16 of the frame's row);
 // the row's lane 0 writes the per-frame scalars and the VAD sigmoid.
@@ -304,63 +310,56 @@ __global__ __launch_bounds__(256) void labels_loss_kernel(const float* __restric
   }
 }
 
-// Labels of frames [t0, t0 + 256) of clip b (get_labels, objective.py:40-76,112-139) with the
-// window of VA probabilities staged in LDS: va[t] = sigmoid(vad_logits[t]) computed here exactly as
-// probs_kernel does (so labels equal those of labels_loss_kernel on probs' vad output), then per
-// thread and bit the same sequential fp32 window sum / len >= thr.  The wave-per-frame kernel above
-// issued its window reads from global memory one after another (~57 us per bench step).
-constexpr int LB_T = 256;
-__global__ __launch_bounds__(LB_T) void labels_lds_kernel(const float* __restrict__ vadl, int Tn, int nl, int4 bf,
-                                                          int nb, float thr, int64_t* __restrict__ labels) {
-  __shared__ float sva[2][LB_T + 128];
-  const int b = blockIdx.y, t0 = blockIdx.x * LB_T, tid = threadIdx.x;
+// probs_kernel plus get_labels (objective.py:40-76,112-139) and loss_vap (reduction none,
+// objective.py:220-243) of frames t < nl, in one launch over (16-frame block, clip): the block
+// stages the VA probabilities of its frames' projection windows in LDS (va[t] = sigmoid(vad
+// logit[t]), the same expression as probs' vad output, so the labels equal those of
+// labels_loss_kernel on that output), lane j < 2 nb of a frame's row forms bit j = c nb + bin with
+// the same sequential fp32 window sum / len >= thr, a ballot gathers the label, and the loss is
+// lse - logit[label] from the softmax's own max / sum.  (A separate labels kernel over 256-frame
+// blocks cost 7.5 us per bench step on the tail, before this kernel.)
+constexpr int PL_F = 16;  // frames per block: one 16-lane row each
+__global__ __launch_bounds__(256) void probs_loss_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
+                                                        int Tn, int nb, int now0, int now1, int fut0, int fut1,
+                                                        int4 bf, float thr, float* __restrict__ probs,
+                                                        float* __restrict__ vad, float* __restrict__ p_now,
+                                                        float* __restrict__ p_future, float* __restrict__ H,
+                                                        int64_t* __restrict__ labels, int nl, float* __restrict__ loss) {
+  __shared__ float sva[2][PL_F + 128];
+  const int b = blockIdx.y, t0 = blockIdx.x * PL_F, tid = threadIdx.x;
   const int bfr[4] = {bf.x, bf.y, bf.z, bf.w};
   int hz = 0;
   for (int i = 0; i < nb; ++i) hz += bfr[i];
-  const int nrow = min(LB_T + hz, Tn - 1 - t0);  // frames t0 + 1 .. used by this block's windows
-  for (int i = tid; i < 2 * nrow; i += LB_T) {
+  const int l16 = tid & 15, row = tid >> 4, t = t0 + row;
+  const int64_t f = (int64_t)b * Tn + t;
+  f32x4 e[4];
+  if (t < Tn) soft16_load(logits + f * 256, l16, e);  // in flight during the window staging
+  const int nrow = min(PL_F + hz, Tn - 1 - t0);  // frames t0 + 1 .. used by this block's windows
+  for (int i = tid; i < 2 * nrow; i += 256) {
     const int r = i >> 1, c = i & 1;
     const float x = vadl[((int64_t)b * Tn + t0 + 1 + r) * 2 + c];
     sva[c][r] = 1.0f / (1.0f + expf(-x));
   }
   __syncthreads();
-  const int t = t0 + tid;
-  if (t >= nl) return;
-  int64_t label = 0;
-  for (int c = 0; c < 2; ++c) {
-    int start = 0;
-    for (int bin = 0; bin < nb; ++bin) {
-      float sm = 0.f;
-      for (int j = 0; j < bfr[bin]; ++j) sm += sva[c][tid + start + j];
-      if ((sm / (float)bfr[bin]) >= thr) label |= (int64_t)1 << (c * nb + bin);
-      start += bfr[bin];
-    }
-  }
-  labels[(int64_t)b * nl + t] = label;
-}
-
-// probs_kernel plus loss_vap (reduction none, objective.py:220-243) of frames t < nl from the
-// labels above: loss = logsumexp(logits) - logits[label], with the softmax's own max / sum
-__global__ __launch_bounds__(256) void probs_loss_kernel(const float* __restrict__ logits, const float* __restrict__ vadl,
-                                                        int Tn, int64_t frames, int nb, int now0, int now1, int fut0,
-                                                        int fut1, float* __restrict__ probs, float* __restrict__ vad,
-                                                        float* __restrict__ p_now, float* __restrict__ p_future,
-                                                        float* __restrict__ H, const int64_t* __restrict__ labels,
-                                                        int nl, float* __restrict__ loss) {
-  const int l16 = threadIdx.x & 15;
-  const int64_t f = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-  if (f >= frames) return;
-  f32x4 e[4];
+  if (t >= Tn) return;  // row-uniform: the DPP reductions stay inside fully active rows
   float mx, sum;
-  soft16(logits + f * 256, l16, e, mx, sum);
+  soft16_exp(e, mx, sum);
   probs_frame(f, l16, e, sum, nb, now0, now1, fut0, fut1, vadl, probs, vad, p_now, p_future, H);
-  if (l16 == 0) {
-    const int64_t b = f / Tn;
-    const int t = (int)(f - b * Tn);
-    if (t < nl) {
-      const int64_t i = b * nl + t;
-      loss[i] = (mx + logf(sum)) - logits[f * 256 + labels[i]];
-    }
+  bool bit = false;
+  if (t < nl && l16 < 2 * nb) {
+    const int c = l16 / nb, bin = l16 - c * nb;
+    int start = 0;
+    for (int i = 0; i < bin; ++i) start += bfr[i];
+    float sm = 0.f;
+    for (int j = 0; j < bfr[bin]; ++j) sm += sva[c][row + start + j];
+    bit = (sm / (float)bfr[bin]) >= thr;
+  }
+  const unsigned long long m = __ballot(bit);
+  if (l16 == 0 && t < nl) {
+    const int64_t label = (int64_t)((m >> (16 * (row & 3))) & ((1ull << (2 * nb)) - 1ull));
+    const int64_t i = (int64_t)b * nl + t;
+    labels[i] = label;
+    loss[i] = (mx + logf(sum)) - logits[f * 256 + label];
   }
 }
 
@@ -544,11 +543,9 @@ hipError_t launch_probs_loss(const float* logits, const float* vad_logits, int B
   }
   const int nl = Tn - horizon;
   if (nl <= 0 || horizon > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(labels_lds_kernel, dim3((unsigned)((nl + LB_T - 1) / LB_T), (unsigned)B), dim3(LB_T), 0, st,
-                     vad_logits, Tn, nl, bf, n_bins, threshold, labels);
-  const int64_t frames = (int64_t)B * Tn;
-  hipLaunchKernelGGL(probs_loss_kernel, dim3((unsigned)((frames + 15) / 16)), dim3(256), 0, st, logits, vad_logits, Tn,
-                     frames, n_bins, now0, now1, fut0, fut1, probs, vad, p_now, p_future, H, labels, nl, loss);
+  hipLaunchKernelGGL(probs_loss_kernel, dim3((unsigned)((Tn + PL_F - 1) / PL_F), (unsigned)B), dim3(256), 0, st, logits,
+                     vad_logits, Tn, n_bins, now0, now1, fut0, fut1, bf, threshold, probs, vad, p_now, p_future, H,
+                     labels, nl, loss);
   return hipGetLastError();
 }
 
