@@ -42,28 +42,54 @@ __global__ __launch_bounds__(256) void lstm_kernel(const float* __restrict__ gx,
     for (int r = 0; r < 4; ++r) c[ut][r] = 0.f;
   __syncthreads();
 
-  const float* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4;
-  const chunk16* wbase = whh + (int64_t)w * 16 * Gm::KG * 64 + lane;
-  for (int t = 0; t < Tn; ++t) {
-    const unsigned char* hcur = hbuf[t & 1];
-    unsigned char* hnext = hbuf[(t + 1) & 1];
-    f32x4 acc[4][4];
-    const float* gxt = gxs + (int64_t)t * G4 + 64 * w + (lane >> 4) * 4;
+  const float* gxs = gx + (int64_t)(valid ? seq : 0) * Tn * G4 + 64 * w + (lane >> 4) * 4;
+  // this wave's packed W_hh fragments through a buffer resource: one lane offset, scalar fragment
+  // offsets (a pointer per fragment would hold 2 VGPRs for each of the 16 KG fragments)
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(whh + (int64_t)w * 16 * Gm::KG * 64, 16u * Gm::KG * 64u * 16u);
+  const uint32_t wlo = (uint32_t)lane * 16u;
+  // W_hh does not change between steps, so its fragments stream through a register ring of PD
+  // k-groups that runs on across the step boundary (the fragments of k-group kg are re-issued as
+  // soon as k-group kg is consumed, for the next step), and the gate rows gx of step t+1 load
+  // while step t computes: no L2 / HBM round trip is exposed per k-group or per step (the
+  // load-then-use form ran ~47 us per step at 2 workgroups per launch).
+  constexpr int KG = Gm::KG, PD = sizeof(T) == 4 ? 4 : 2;  // fp32: 465 registers, no spills
+  static_assert(KG % PD == 0, "the ring slot of a k-group must repeat across steps");
+  chunk16 wr[PD][16];
+  auto wload = [&](int kg, chunk16(&r)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = buf_load16(rw, wlo, (uint32_t)((i * KG + kg) * 64 * 16));
+  };
+#pragma unroll
+  for (int p = 0; p < PD; ++p) wload(p, wr[p]);
+  f32x4 gxn[4][4];
+  auto gxload = [&](int t) {
+    const float* gxt = gxs + (int64_t)t * G4;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int ut = 0; ut < 4; ++ut)
-        acc[g][ut] = valid ? *(const f32x4*)(gxt + g * HD + ut * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int kg = 0; kg < Gm::KG; ++kg) {
+        gxn[g][ut] = valid ? *(const f32x4*)(gxt + g * HD + ut * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  gxload(0);
+  for (int t = 0; t < Tn; ++t) {
+    const unsigned char* hcur = hbuf[t & 1];
+    unsigned char* hnext = hbuf[(t + 1) & 1];
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ut = 0; ut < 4; ++ut) acc[g][ut] = gxn[g][ut];
+    gxload(t + 1 < Tn ? t + 1 : t);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
       const chunk16 hb = *(const chunk16*)(hcur + (lane & 15) * Gm::HROW + (kg * 4 + (lane >> 4)) * 16);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int ut = 0; ut < 4; ++ut) {
-          const chunk16 a = wbase[((g * 4 + ut) * Gm::KG + kg) * 64];
-          acc[g][ut] = mfma_chunk<T>(a, hb, acc[g][ut]);
-        }
+        for (int ut = 0; ut < 4; ++ut) acc[g][ut] = mfma_chunk<T>(wr[kg % PD][g * 4 + ut], hb, acc[g][ut]);
+      wload((kg + PD) % KG, wr[kg % PD]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the ring: no load hoisted past its k-group
     }
     // cell update: unit u = 64w + 16ut + (lane>>4)*4 + r, sequence lane&15
 #pragma unroll
