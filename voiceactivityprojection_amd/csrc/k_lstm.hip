@@ -25,6 +25,9 @@ struct LstmGeom {
   static constexpr int HROW = HD * sizeof(T) + 16;  // padded LDS row bytes
 };
 
+VAP_DEV float cell_sig(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+VAP_DEV float cell_tanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
+
 template <typename T>
 __global__ __launch_bounds__(256) void lstm_kernel(const float* __restrict__ gx, int S, int Tn,
                                                   const chunk16* __restrict__ whh, T* __restrict__ out,
@@ -96,13 +99,13 @@ __global__ __launch_bounds__(256) void lstm_kernel(const float* __restrict__ gx,
     for (int ut = 0; ut < 4; ++ut) {
       float h[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ig = 1.0f / (1.0f + expf(-acc[0][ut][r]));
-        const float fg = 1.0f / (1.0f + expf(-acc[1][ut][r]));
-        const float gg = tanhf(acc[2][ut][r]);
-        const float og = 1.0f / (1.0f + expf(-acc[3][ut][r]));
+      for (int r = 0; r < 4; ++r) {  // v_exp / v_rcp forms (abs. error ~2e-7; libm expf / tanhf cost ~4 us a step)
+        const float ig = cell_sig(acc[0][ut][r]);
+        const float fg = cell_sig(acc[1][ut][r]);
+        const float gg = cell_tanh(acc[2][ut][r]);
+        const float og = cell_sig(acc[3][ut][r]);
         c[ut][r] = fg * c[ut][r] + ig * gg;
-        h[r] = og * tanhf(c[ut][r]);
+        h[r] = og * cell_tanh(c[ut][r]);
       }
       const int u = 64 * w + 16 * ut + (lane >> 4) * 4;
       store4((T*)(hnext + (lane & 15) * Gm::HROW) + u, h[0], h[1], h[2], h[3]);
