@@ -61,15 +61,40 @@ def class_flops(B: int, n: int, heads: int = 4, channel_layers: int = 1, cross_l
     return f, L
 
 
+def host_cpu_share():
+    """The host CPUs this process may use: min(affinity mask, cgroup cpu.max quota, OMP_NUM_THREADS when
+    the environment sets it).  On the GPU pool ``nproc`` shows the whole 256-CPU host, which the
+    node's GPU jobs share; the pool grants 16 CPUs per GPU and sets OMP_NUM_THREADS=16, asking jobs to
+    keep it, so the CPU baseline runs on exactly that share."""
+    nproc = os.cpu_count() or 1
+    share, src = nproc, "os.cpu_count"
+    try:
+        aff = len(os.sched_getaffinity(0))
+        if aff < share:
+            share, src = aff, "sched_getaffinity"
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(per) > 0 and int(int(q) / int(per)) < share:
+            share, src = max(1, int(int(q) / int(per))), "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < share:
+        share, src = int(omp), "OMP_NUM_THREADS (the pool's per-GPU CPU share)"
+    return share, nproc, src
+
+
 def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int = 32, batch: int = 4):
     """Time the CPU oracle (torch fp32 restatement of the reference) on a bounded sample: batches of
     `batch` clips of the workload's length (the GPU workload's shape, fewer clips per call) until the
-    budget is spent."""
+    budget is spent, on every host CPU this process may use (host_cpu_share)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import vap_oracle as O
     from voiceactivityprojection_amd.weights import synthetic_waveform
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, nproc, share_src = host_cpu_share()
     torch.set_num_threads(threads)
     sd = O.state_dict_to_torch(sd_np)
     n = int(seconds * 16000)
@@ -84,9 +109,9 @@ def cpu_baseline(seconds: float, sd_np, budget_s: float = 12.0, max_clips: int =
             break
     el = time.perf_counter() - t0
     return {"value": round(done * seconds / el, 3), "unit": "audio-s/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(),
+            "nproc": nproc, "cores_source": share_src,
             "sample": f"{calls} call(s) of {batch} x {seconds:g} s stereo clips, oracle/vap_oracle.py fp32 on "
-                      f"{threads} host threads ({el:.1f} s; nproc {os.cpu_count()})"}
+                      f"{threads} host threads = this process's CPU share ({share_src}; {el:.1f} s; nproc {nproc})"}
 
 
 def parse_args(argv=None):
@@ -106,7 +131,13 @@ def parse_args(argv=None):
     # pair splits the two front-end streams' overlap); the last timed step carries them by default
     ap.add_argument("--roofline-events", type=int, default=1,
                     help="timed steps (the last ones) whose dominant-kernel launches carry HIP events (-1: all)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary configurations measured after the headline at N=1 (C4, parity mode)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
+    # tests: rank 1 of the stub writes clips shifted by one (the exact gather check must catch it)
+    ap.add_argument("--stub-wrong-offset", action="store_true", help=argparse.SUPPRESS)
+    # tests: the handle never publishes the recurrence's ready flag of this time chunk (vap_test_drop_ready)
+    ap.add_argument("--test-drop-ready", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -166,6 +197,7 @@ def run_rank(args) -> int:
 
     from voiceactivityprojection_amd.distributed import PackedOutputs, gather_packed
     from voiceactivityprojection_amd.utils import frame_lengths
+    from voiceactivityprojection_amd.weights import synthetic_batch
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if args.stub:
@@ -182,16 +214,20 @@ def run_rank(args) -> int:
     T = frame_lengths(n)[5]
     keys = ("probs", "vad", "p_now", "p_future", "H", "loss") if args.gather == "all" else ("p_now", "p_future", "vad", "H")
     if args.stub:
-        model, wav, sd_np = _StubModel(rank * B), None, None
+        model, wav, sd_np = _StubModel(rank * B + (1 if args.stub_wrong_offset and rank == 1 else 0)), None, None
     else:
         from vap.model import VapGPT
-        from voiceactivityprojection_amd.weights import synthetic_batch, synthetic_state_dict
+        from voiceactivityprojection_amd.weights import synthetic_state_dict
 
         sd_np = synthetic_state_dict(seed=0)
         model = VapGPT(precision=args.precision)
         model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
         model = model.to(dev).eval()
         wav = torch.from_numpy(synthetic_batch(rank * B, B, n)).to(dev)
+        if args.test_drop_ready >= 0:
+            from voiceactivityprojection_amd import _native as N0
+
+            N0.check(N0.lib().vap_test_drop_ready(model._native(dev), args.test_drop_ready))
 
     # double-buffered packed outputs: step i writes packs[i % 2] while the gather of step i - 1 runs
     packs = [PackedOutputs(B, T, dev, keys) for _ in range(2)]
@@ -287,20 +323,34 @@ def run_rank(args) -> int:
     gather_info = None
     if dist:
         last = (state["i"] - 1) % 2
-        verified = None
+        verified, checked = None, []
         if rank == 0:
             got = recvs[last]
             verified = bool(torch.equal(got[0], packs[last].flat))  # rank 0's own shard, bit for bit
-            if args.stub:  # every rank's region holds exactly its clips' tags
-                for r in range(world):
-                    exp = _StubModel(r * B).probs(None, PackedOutputs(B, T, "cpu", keys).views())
-                    view = packs[last].views(B, flat=got[r])
-                    verified = verified and all(torch.equal(view[k], exp[k]) for k in keys)
-            else:
-                verified = verified and all(bool(torch.isfinite(g).all()) for g in got)
+            verified = verified and all(bool(torch.isfinite(g).all()) for g in got)
+            # every rank's first and last clip recomputed here, ALONE (clip seed = global clip index), and
+            # compared bit for bit with that rank's gathered region: batch invariance (every kernel is per
+            # sequence) makes a one-clip run exact, so a rank that computed the wrong clips fails here
+            one = PackedOutputs(1, T, dev, keys)
+            for r in range(world):
+                view = packs[last].views(B, flat=got[r])
+                for i in sorted({0, B - 1}):
+                    c = r * B + i
+                    if args.stub:
+                        _StubModel(c).probs(None, one.views())
+                    else:
+                        model.probs(torch.from_numpy(synthetic_batch(c, 1, n)).to(dev), out=one.views())
+                    ok = all(torch.equal(view[k][i:i + 1], one.views()[k]) for k in keys)
+                    checked.append({"rank": r, "clip": c, "bit_identical": ok})
+                    verified = verified and ok
+            if not args.stub:
+                model.synchronize()
         gather_info = {"collective": "torch.distributed.gather" + (" (gloo)" if args.stub else " (RCCL)"),
                        "calls_per_step": 1, "bytes_per_rank": packs[0].flat.numel() * 4, "keys": list(keys),
-                       "overlapped_with_next_step": True, "verified": verified}
+                       "overlapped_with_next_step": True, "verified": verified,
+                       "verification": "rank 0's shard bit for bit; every rank's first and last clip recomputed "
+                                       "alone on rank 0 and compared bit for bit (batch invariance)",
+                       "clips_checked": checked}
 
     if rank == 0:
         audio_s = world * B * args.seconds * args.steps
@@ -358,6 +408,14 @@ def run_rank(args) -> int:
                                       "the back end in two clip halves on two streams; a back-end class is timed in "
                                       "a forward with the back end on one stream")
             line["model_tflops_per_s"] = round(sum(flops.values()) * args.steps * world / el / 1e12, 2)
+        if world == 1 and not args.stub:
+            # the headline outputs of the last timed step against the reference's own outputs for clips
+            # 0..3 of this batch (tests/golden/bench4_20s.npz), at the mode's stated tolerance
+            fx = fixture_errors(packs[(state["i"] - 1) % 2].views(), B, args.seconds, args.precision)
+            if fx is not None:
+                line["parity"] = fx
+            if not args.no_extras:
+                line["extras"] = extras(args, model, dev, sd_np)
         if world == 1 and not args.no_cpu_baseline and not args.stub:
             line["cpu_baseline"] = cpu_baseline(args.seconds, sd_np)
         else:
@@ -365,7 +423,79 @@ def run_rank(args) -> int:
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+    if gather_info is not None and rank == 0 and gather_info["verified"] is not True:
+        print("bench.py: the gathered outputs failed the exact per-rank check", file=sys.stderr)
+        return 3
     return 0
+
+
+def fixture_errors(out, B: int, seconds: float, precision: str):
+    """Max abs error of clips 0..3 of a bench batch (synthetic_batch(0, ...), 20 s) against the reference's
+    outputs for the same clips (tests/golden/bench4_20s.npz, tools/gen_golden.py), per output, with the
+    mode's stated tolerance (voiceactivityprojection_amd/tolerances.py)."""
+    from voiceactivityprojection_amd.tolerances import TOL
+
+    path = os.path.join(REPO, "tests", "golden", "bench4_20s.npz")
+    if seconds != 20.0 or B < 4 or not os.path.exists(path):
+        return None
+    g = dict(np.load(path, allow_pickle=False))
+    tol = TOL[precision]
+    err = {}
+    for k in ("vad", "p_now", "p_future", "H", "loss"):
+        if k in out and k in g:
+            err[k] = float(np.abs(out[k][:4].float().cpu().numpy() - g[k]).max())
+    if "probs" in out and "probs_stride10" in g:
+        err["probs"] = float(np.abs(out["probs"][:4, ::10].float().cpu().numpy() - g["probs_stride10"]).max())
+    return {"reference_fixture": "tests/golden/bench4_20s.npz (clips 0..3 of this batch, reference outputs)",
+            "max_abs_err": {k: float(f"{v:.3g}") for k, v in err.items()}, "tolerance": {k: tol[k] for k in err},
+            "within_tolerance": all(err[k] <= tol[k] for k in err)}
+
+
+def _leg(model, wav, steps: int, warmup: int, keys=None):
+    """Steps of model.probs on a resident batch: (ms per step, outputs of the last step)."""
+    out = None
+    for _ in range(warmup):
+        out = model.probs(wav)
+    torch.cuda.synchronize()
+    model.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = model.probs(wav)
+    torch.cuda.synchronize()
+    model.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3, out
+
+
+def extras(args, model, dev, sd_np, steps: int = 3, warmup: int = 2):
+    """Secondary BASELINE configurations measured in the same run after the headline (N = 1, untimed by
+    the headline): C4 (32 x 60 s, T = 3000, the headline's precision) and the fp32 parity mode on the
+    headline workload (64 x 20 s) with its errors against the reference fixture."""
+    from vap.model import VapGPT
+    from voiceactivityprojection_amd.weights import synthetic_batch
+
+    res = {}
+    n4, B4 = 60 * 16000, 32
+    wav4 = torch.from_numpy(synthetic_batch(0, B4, n4)).to(dev)
+    ms, _ = _leg(model, wav4, steps, warmup)
+    res["c4"] = {"value": round(B4 * 60.0 / (ms * 1e-3), 2), "unit": "audio-s/s", "ms_per_step": round(ms, 3),
+                 "steps": steps, "warmup": warmup, "dtype": args.precision,
+                 "config": "BASELINE.json configs[3]: batch=32 x 60s stereo @16kHz (T=3000, AliBi extrapolation), "
+                           "1 GPU, VapGPT.probs"}
+    del wav4
+    if args.precision != "fp32":
+        B, n = args.batch, int(args.seconds * 16000)
+        m32 = VapGPT(precision="fp32")
+        m32.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+        m32 = m32.to(dev).eval()
+        wav = torch.from_numpy(synthetic_batch(0, B, n)).to(dev)
+        ms, out = _leg(m32, wav, steps, warmup)
+        res["parity_mode"] = {"value": round(B * args.seconds / (ms * 1e-3), 2), "unit": "audio-s/s",
+                              "ms_per_step": round(ms, 3), "steps": steps, "warmup": warmup, "dtype": "fp32",
+                              "config": f"the headline workload (batch={B} x {args.seconds:g}s) in the fp32 parity mode",
+                              "parity": fixture_errors(out, B, args.seconds, "fp32")}
+        del m32, wav, out
+    torch.cuda.empty_cache()
+    return res
 
 
 if __name__ == "__main__":

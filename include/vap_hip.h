@@ -226,6 +226,12 @@ int vap_test_plan(const vap_handle* h, int batch, int64_t n_samples, int64_t* ou
 /* pair-recurrence exchange tag counter of a handle (tests): *get = the last tag issued; set >= 0 moves it (e.g.
  * next to the 32-bit wrap, which the next launch handles by clearing the exchange slots) */
 int vap_test_xtag(vap_handle* h, int64_t set, int64_t* get);
+/* robustness tests: from now on the handle never publishes the recurrence's ready flag of time chunk `chunk`
+ * (-1: publish all again), so the bounded wait times out and the hand-off error surfaces */
+int vap_test_drop_ready(vap_handle* h, int chunk);
+/* pair-recurrence exchange store policy of a handle (VAP_LSTM_XPLAIN at vap_create): 0 by XCD handshake,
+ * 1 plain (L2) stores always, -1 write-through always */
+int vap_test_lstm_xplain(vap_handle* h, int policy);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled conv01 workgroups (VAP_CONV01_STAMPS=1) */
 int vap_test_read_stamps(unsigned long long* out);
 /* timing diagnostics: 8 x 24 s_memtime stamps of sampled fused-block workgroups (VAP_BLOCK_STAMPS=1) */

@@ -31,3 +31,20 @@ def sd_np():
     from voiceactivityprojection_amd.weights import synthetic_state_dict
 
     return synthetic_state_dict(seed=0)
+
+
+@pytest.fixture
+def drop_ready(monkeypatch):
+    """Robustness tests: every native handle a VapGPT creates from now on never publishes the recurrence's
+    ready flag of time chunk 1 (test ABI vap_test_drop_ready), so the bounded hand-off wait times out."""
+    from voiceactivityprojection_amd import _native as N
+    from voiceactivityprojection_amd.model import VapGPT
+
+    orig = VapGPT._native
+
+    def patched(self, device):
+        h = orig(self, device)
+        N.check(N.lib().vap_test_drop_ready(h, 1), "vap_test_drop_ready")
+        return h
+
+    monkeypatch.setattr(VapGPT, "_native", patched)

@@ -82,7 +82,7 @@ class _OracleModel:
     sample_rate, frame_hz, horizon_time = 16000, 50, 2.0
 
     class objective:
-        n_classes = 256
+        n_classes, horizon = 256, 100
 
     def __init__(self, sd):
         self.sd = sd
@@ -149,3 +149,45 @@ def test_empty_shards_join_the_gather():
     for k in ("probs", "p_now", "p_future", "vad", "H", "loss"):
         assert got[0][1][k].shape == tuple(ref[k].shape)
         np.testing.assert_allclose(got[0][1][k], ref[k].numpy(), atol=1e-5, rtol=1e-5)
+
+
+class _ShapeModel:
+    """probs() with the engine's strict `out` checks (VapGPT.probs: loss is (B, T - objective.horizon)) and
+    the reference objective for any bin_times; writes clip-tagged values."""
+
+    sample_rate, frame_hz = 16000, 50
+
+    def __init__(self, bin_times):
+        from voiceactivityprojection_amd.objective import ObjectiveVAP
+
+        self.objective = ObjectiveVAP(bin_times=bin_times, frame_hz=50)
+        self.horizon_time = self.objective.horizon_time
+
+    def probs(self, w, out):
+        from voiceactivityprojection_amd.utils import frame_lengths
+
+        B, T = w.shape[0], frame_lengths(w.shape[-1])[-1]
+        shapes = {"probs": (B, T, 256), "vad": (B, T, 2), "p_now": (B, T, 2), "p_future": (B, T, 2), "H": (B, T),
+                  "loss": (B, T - self.objective.horizon)}
+        for k, v in out.items():
+            if tuple(v.shape) != shapes[k]:
+                raise ValueError(f"out[{k!r}] must be {shapes[k]}, got {tuple(v.shape)}")
+            v.copy_(w[:, :1, :1].reshape(B, *([1] * (v.dim() - 1))).expand_as(v))
+        return out
+
+
+def test_probs_sharded_non_whole_frame_bins():
+    """bin_times that are not whole frames (0.15 s, 0.35 s at 50 Hz: 7 and 17 frames, horizon 94, while
+    round(horizon_time * frame_hz) = 95): the packed `loss` region must follow objective.horizon."""
+    port = _free_port()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        m = _ShapeModel([0.15, 0.35, 0.6, 0.8])
+        assert m.objective.horizon == 94 and round(m.horizon_time * m.frame_hz) == 95
+        w = torch.arange(3, dtype=torch.float32).view(3, 1, 1).expand(3, 2, 48000).contiguous()
+        res = probs_sharded(m, w, 0, 1, "cpu")
+        T = 150
+        assert res["loss"].shape == (3, T - 94) and res["probs"].shape == (3, T, 256)
+        assert torch.equal(res["H"][:, 0], torch.arange(3, dtype=torch.float32))
+    finally:
+        dist.destroy_process_group()

@@ -47,8 +47,8 @@ def test_run_py_example_wav(tmp_path, golden, precision, tol):
     print(f"run.py example wav {precision} max abs err:", errs)
 
 
-def test_run_py_raises_on_dropped_handoff(tmp_path, monkeypatch):
-    """A recurrence hand-off that times out (test hook VAP_TEST_DROP_READY) makes run.main raise
+def test_run_py_raises_on_dropped_handoff(tmp_path, drop_ready):
+    """A recurrence hand-off that times out (test ABI vap_test_drop_ready) makes run.main raise
     instead of writing a JSON of invalid outputs."""
     import run
     from scipy.io import wavfile
@@ -57,7 +57,6 @@ def test_run_py_raises_on_dropped_handoff(tmp_path, monkeypatch):
     path = str(tmp_path / "five_s.wav")
     wavfile.write(path, 16000, (wav.T * 32767).astype(np.int16))
     out_json = str(tmp_path / "five_s.json")
-    monkeypatch.setenv("VAP_TEST_DROP_READY", "1")
     with pytest.raises(RuntimeError, match="timed out"):
         run.main(["-a", path, "-sd", "synthetic", "-f", out_json, "--precision", "bf16"])
     assert not os.path.exists(out_json)
@@ -65,20 +64,19 @@ def test_run_py_raises_on_dropped_handoff(tmp_path, monkeypatch):
 
 def test_bench_raises_on_dropped_handoff():
     """bench.py fails (non-zero exit, the hand-off error on stderr) rather than printing a number."""
-    env = dict(os.environ, VAP_TEST_DROP_READY="1")
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "2", "--seconds", "5",
-                        "--steps", "1", "--warmup", "1", "--no-cpu-baseline"], cwd=REPO, env=env,
+                        "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-extras",
+                        "--test-drop-ready", "1"], cwd=REPO,
                        capture_output=True, text=True, timeout=240)
     assert p.returncode != 0 and "timed out" in p.stderr, (p.returncode, p.stdout[-500:], p.stderr[-2000:])
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
 
 
-def test_stream_push_raises_on_dropped_handoff(monkeypatch):
+def test_stream_push_raises_on_dropped_handoff(drop_ready):
     """VapStream.push checks its hand-off by default (the real-time loop never gets an invalid hop)."""
     from vap.model import VapGPT
     from voiceactivityprojection_amd.weights import synthetic_state_dict
 
-    monkeypatch.setenv("VAP_TEST_DROP_READY", "1")
     m = VapGPT(precision="bf16")
     m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed=0).items()}, strict=True)
     m = m.to("cuda").eval()

@@ -16,11 +16,11 @@ from voiceactivityprojection_amd.weights import synthetic_state_dict, synthetic_
 
 pytestmark = pytest.mark.gpu
 
-FP32_TOL = {"probs": 1e-4, "vad": 1e-4, "p_now": 1e-4, "p_future": 1e-4, "H": 1e-3, "loss": 1e-3}
-# bf16 perf mode: <= 3x the largest error measured against the reference fixtures (tools/bf16_errors.py,
-# profiles/r3_bf16_errors.json: probs 1.42e-3, vad 1.34e-2, p_now 5.5e-4, p_future 4.8e-4, H 8.9e-3,
-# loss 1.61e-2 over short_clip, example_wav, len_*, batch_20s, bench4_20s, long_60s)
-BF16_TOL = {"probs": 4e-3, "vad": 3e-2, "p_now": 1.5e-3, "p_future": 1.4e-3, "H": 2.5e-2, "loss": 4.5e-2}
+# the stated tolerances (voiceactivityprojection_amd/tolerances.py): fp32 1e-4 / 1e-3; bf16 <= 3x the largest
+# error measured against the reference fixtures (tools/bf16_errors.py, profiles/r3_bf16_errors_s2.json:
+# probs 1.42e-3, vad 1.34e-2, p_now 5.5e-4, p_future 4.8e-4, H 8.9e-3, loss 1.61e-2 over short_clip,
+# example_wav, len_*, batch_20s, bench4_20s, long_60s)
+from voiceactivityprojection_amd.tolerances import BF16_TOL, FP32_TOL  # noqa: E402
 
 
 def _model(precision="fp32", lstm_layers=1):
@@ -224,7 +224,7 @@ def test_encoder_bf16_vs_reference(m16, golden):
     for got, exp in ((x1, g["enc1"]), (x2, g["enc2"])):
         err = (got.cpu().numpy() - exp).__abs__().max()
         print("bf16 encoder max abs err:", err)
-        assert err < 0.08, f"bf16 encoder max abs err {err}"
+        assert err < 0.06, f"bf16 encoder max abs err {err}"  # <= 3x the measured 2.12e-2 (r4s2)
 
 
 def test_long_60s_bf16(m16, golden):
@@ -342,7 +342,7 @@ def test_attention_maps_bf16_vs_oracle(m16):
         assert got.shape == exp.shape, (k, got.shape, exp.shape)
         err = float(np.abs(got - exp).max())
         print(f"bf16 attention map {k} max abs err:", err)
-        assert err < 3e-2, f"{k}: {err}"
+        assert err < 1.9e-2, f"{k}: {err}"  # <= 3x the largest measured (cross_attn 6.3e-3, r4s2)
 
 
 @pytest.mark.parametrize("B,T", [(3, 130), (2, 1000), (1, 101)])

@@ -68,11 +68,10 @@ def test_batch_at_and_above_default_cap():
         torch.cuda.empty_cache()
 
 
-def test_handoff_timeout_is_reported(monkeypatch):
-    """A ready flag that never arrives (test hook VAP_TEST_DROP_READY) makes the recurrence's bounded
+def test_handoff_timeout_is_reported(drop_ready):
+    """A ready flag that never arrives (test ABI vap_test_drop_ready) makes the recurrence's bounded
     wait give up after ~2 s: synchronize() raises, and so does the next forward if not checked; the
     word is cleared once reported."""
-    monkeypatch.setenv("VAP_TEST_DROP_READY", "1")
     m = _model()
     w = _batch(2, 80000, 50)  # 5 s: T = 250, several time chunks
     m(w)
@@ -155,13 +154,18 @@ def test_bf16_repeat_determinism_and_xcd_handshake():
         assert l2 == int(own == partner), (own, partner, l2)
 
 
-def test_exchange_policy_does_not_change_outputs(monkeypatch):
+def test_exchange_policy_does_not_change_outputs():
     """The pair recurrence's h exchange policy (XCD-local L2 by handshake, forced write-through with
-    VAP_LSTM_XPLAIN=-1) changes where the bytes travel, not the arithmetic: outputs bit-identical."""
+    vap_test_lstm_xplain -1) changes where the bytes travel, not the arithmetic: outputs bit-identical."""
+    import ctypes
+
+    from voiceactivityprojection_amd import _native as N
+
     m = _model()
     w = _batch(3, 160000, 77)
     ref = m.probs(w)
-    monkeypatch.setenv("VAP_LSTM_XPLAIN", "-1")
+    h = m._native(torch.device("cuda", torch.cuda.current_device()))
+    N.check(N.lib().vap_test_lstm_xplain(h, -1))
     out = m.probs(w)
     m.synchronize()
     for k in ref:

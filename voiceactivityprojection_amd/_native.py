@@ -68,6 +68,8 @@ _SIGS = {
     "vap_synchronize": (ctypes.c_int, [_P, _P]),
     "vap_test_plan": (ctypes.c_int, [_P, ctypes.c_int, _I64, _P]),
     "vap_test_xtag": (ctypes.c_int, [_P, _I64, ctypes.POINTER(_I64)]),
+    "vap_test_drop_ready": (ctypes.c_int, [_P, ctypes.c_int]),
+    "vap_test_lstm_xplain": (ctypes.c_int, [_P, ctypes.c_int]),
     "vap_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "vap_timing_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "vap_test_gemm": (ctypes.c_int, [ctypes.c_int, _P, _I64, _I64, _P, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,

@@ -854,7 +854,8 @@ size_t lstm_pair_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * P_SLOT
 int lstm_pair_workgroups(int S) { return 2 * ((S + NS - 1) / NS); }
 
 hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out,
-                            int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag) {
+                            int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag,
+                            int xplain) {
   if (S <= 0 || Tn <= 0 || seq0 < 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn > 0xFFFFFFFFull)
     return hipErrorInvalidValue;
   LstmSync sy{};
@@ -867,9 +868,7 @@ hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16*
     sy = *sync;
   }
   sy.xtag = xtag;
-  const char* xpe = getenv("VAP_LSTM_XPLAIN");  // read per launch (tests switch it)
-  const int xplain = xpe ? atoi(xpe) : 0;
-  sy.xplain = xplain;
+  sy.xplain = xplain;  // the handle's exchange-store policy (vap_create / vap_test_lstm_xplain)
   static const int hot = getenv("VAP_LSTM_HANDOFF") ? atoi(getenv("VAP_LSTM_HANDOFF")) : 0;  // diagnostics
   sy.handoff_trace = hot;
   static const int st0 = getenv("VAP_LSTM_STAMP_T0") ? atoi(getenv("VAP_LSTM_STAMP_T0")) : 100;

@@ -63,8 +63,8 @@ struct vap_handle {
   // pieces 0.1 / 0.27 / 0.48 / 0.72 in a same-box A/B: a smaller last piece shortens what the recurrence
   // still has to do after the front end's end)
   std::vector<double> tc_fe{0.12, 0.3, 0.5, 0.7, 0.85}, tc_be{0.64};
-  bool tc_be_auto = true;
-  bool tc_fe_auto = true;  // + a 120-frame first front-end piece for clips longer than 1200 frames  // back-end chunks of clips longer than 1200 frames by rule (tc_schedule_split)
+  bool tc_be_auto = true;  // back-end chunks of clips longer than 1200 frames by rule (tc_schedule_split)
+  bool tc_fe_auto = true;  // + a 120-frame first front-end piece for clips longer than 1200 frames
   bool heads_chunked = true;  // VAP_HEADS_CHUNKED=0: heads once after the last back-end chunk (per chunk,
                               // the fused heads kernel takes the first chunk's heads off the tail after
                               // the recurrence, which binds since the caller stream has ~0.2 ms of slack)
@@ -100,7 +100,8 @@ struct vap_handle {
   // exchange tags: every pair-recurrence launch takes the next Tn + 1 values (strictly increasing, so a
   // slot left by any earlier launch never holds a tag a later launch waits for); wraps by clearing xbuf
   unsigned xtag = 0;
-  int test_drop_ready = -1;  // VAP_TEST_DROP_READY=c (tests only): never publish ready[c] -> the wait times out
+  int test_drop_ready = -1;  // tests only (vap_test_drop_ready): never publish ready[c] -> the wait times out
+  int lstm_xplain = 0;       // VAP_LSTM_XPLAIN / vap_test_lstm_xplain: pair-exchange store policy (0 = by handshake)
   int lstm_max_wg = 0;  // VAP_LSTM_MAX_WG: persistent recurrence launches at most this many workgroups
   unsigned epoch = 0;
   unsigned done_expect[MAXMB] = {};
@@ -1088,7 +1089,7 @@ int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer
   const unsigned tag0 = h->xtag + 1;  // this launch: tags tag0 .. tag0 + L4
   h->xtag += (unsigned)span;
   HIPCHK(launch_lstm_pair(GX, seq0, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
-                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0));
+                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0, h->lstm_xplain));
   return VAP_OK;
 }
 
@@ -1893,10 +1894,17 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_TIME_CHUNKS")) h->time_chunks = atoi(e);
   if (const char* e = getenv("VAP_FE_STREAMS")) h->fe_streams = atoi(e);
   if (const char* e = getenv("VAP_LSTM_MAX_WG")) h->lstm_max_wg = atoi(e);
-  if (const char* e = getenv("VAP_TEST_DROP_READY")) h->test_drop_ready = atoi(e);
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
   if (const char* e = getenv("VAP_BE_SPLIT")) h->be_split = atoi(e);
-  if (const char* e = getenv("VAP_BE_FRAC")) h->be_frac = atof(e);
+  if (const char* e = getenv("VAP_LSTM_XPLAIN")) h->lstm_xplain = atoi(e);
+  if (const char* e = getenv("VAP_BE_FRAC")) {  // the caller stream's share of two back-end groups, in (0, 1)
+    const double f = atof(e);
+    if (!(f > 0.0 && f < 1.0)) {
+      delete h;
+      return fail(VAP_ERR_INVALID, "VAP_BE_FRAC must be a number in (0, 1)");
+    }
+    h->be_frac = f;
+  }
   auto parse_list = [](const char* e, std::vector<double>& out) {
     out.clear();
     std::string v = e;
@@ -2257,6 +2265,19 @@ int vap_test_xtag(vap_handle* h, int64_t set, int64_t* get) {
     if (set > 0xFFFFFFFFll) return fail(VAP_ERR_INVALID, "tag out of range");
     h->xtag = (unsigned)set;
   }
+  return VAP_OK;
+}
+
+int vap_test_drop_ready(vap_handle* h, int chunk) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  h->test_drop_ready = chunk < 0 ? -1 : chunk;
+  return VAP_OK;
+}
+
+int vap_test_lstm_xplain(vap_handle* h, int policy) {
+  if (!h) return fail(VAP_ERR_INVALID, "null handle");
+  if (policy < -1 || policy > 1) return fail(VAP_ERR_INVALID, "policy must be -1, 0 or 1");
+  h->lstm_xplain = policy;
   return VAP_OK;
 }
 

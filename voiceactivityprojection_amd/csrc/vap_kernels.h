@@ -138,7 +138,8 @@ hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t 
 // differ between launches that share the buffer), and the workgroups one launch runs
 // gx: the pair-layout gate buffer (gx_pair_block) whose sequence seq0 is this launch's sequence 0
 hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
-                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag);
+                            hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag,
+                            int xplain = 0);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
 // The bf16 LSTM gate buffer in the pair-recurrence layout (k_lstm.hip lstm_pair_kernel): for each group of

@@ -141,7 +141,7 @@ def probs_sharded(model, waveform_global: torch.Tensor, rank: int, world: int, d
     sizes = shard_sizes(gb, world)
     s, e = shard_range(gb, rank, world)
     T = frame_lengths(waveform_global.shape[-1])[-1]
-    horizon = int(round(model.horizon_time * model.frame_hz))
+    horizon = int(model.objective.horizon)  # sum of the truncated bin frames, as probs() sizes `loss`
     packed = PackedOutputs(max(sizes), T, device, keys, model.objective.n_classes, horizon)
     packed.flat.zero_()
     if e > s:
