@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-PREC = {"fp32": (0, torch.float32), "bf16": (1, torch.bfloat16)}
+PREC = {"fp32": (0, torch.float32), "bf16": (1, torch.bfloat16), "split": (2, torch.float32)}
 
 
 def lib():
@@ -35,13 +35,15 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "split"])
 @pytest.mark.parametrize("case", ["plain", "conv_cn_relu", "resid", "ln_gelu", "gelu", "comb", "many_tiles",
                                   "many_tiles_n1024"])
 def test_gemm(prec, case):
     """Implicit-conv GEMM with every epilogue form.  comb = act(LN(A W)) + residual (the combinator's
     second half); many_tiles* = more 256-row tiles than CUs, so persistent workgroups walk several
-    tiles with the DMA stream running across the tile seams (N 256 and N 1024)."""
+    tiles with the DMA stream running across the tile seams (N 256 and N 1024).  split = the fp32 parity
+    mode's kernel (fp32 operands as hi + lo bf16 pairs, three bf16 MFMAs per tile-step): fp32 accuracy
+    to ~2^-16 of a product, checked at 3e-5 of the output scale."""
     N = lib()
     code, dt = PREC[prec]
     g = torch.Generator().manual_seed(1)
@@ -91,7 +93,7 @@ def test_gemm(prec, case):
         ref = F.gelu(ref)
     if use_add:
         ref = ref + add
-    out_f32 = 1 if (prec == "fp32" or case in ("resid", "ln_gelu", "comb")) else 0
+    out_f32 = 1 if (prec != "bf16" or case in ("resid", "ln_gelu", "comb")) else 0
     C = torch.zeros(S, Mps, Nn, device="cuda", dtype=torch.float32 if out_f32 else dt)
     Ad, Wd = Aq.cuda(), Wq.cuda()
     bd, gd, bed, addd = bias.cuda(), gamma.cuda(), beta.cuda(), add.cuda()
@@ -99,7 +101,7 @@ def test_gemm(prec, case):
          Mps, S, _p(C), Nn, Mps * Nn, _p(addd) if use_add else None, Nn, Mps * Nn, _p(gd), _p(bed), norm, act,
          out_f32, _st())
     got = C.float().cpu()
-    tol = 2e-4 if prec == "fp32" else (1e-2 if not out_f32 else 3e-3)
+    tol = {"fp32": 2e-4, "split": 3e-5}.get(prec, 1e-2 if not out_f32 else 3e-3)
     err = (got - ref).abs().max().item()
     scale = ref.abs().max().item()
     assert err <= tol * max(1.0, scale), f"{prec}/{case}: max err {err} (scale {scale})"
@@ -139,7 +141,7 @@ def test_convk4(S, L_in, a, b):
     assert torch.all(got[:, M:] == 7.0), "rows past the range were written"
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "split"])
 @pytest.mark.parametrize("kv_swap", [0, 1])
 def test_attention(prec, kv_swap):
     N = lib()
@@ -165,18 +167,20 @@ def test_attention(prec, kv_swap):
     att = (att + bias).masked_fill(mask, float("-inf")).softmax(-1)
     ref = (att @ v).transpose(1, 2).reshape(S, T, D)
     err = (O.float().cpu() - ref).abs().max().item()
-    tol = 2e-5 if prec == "fp32" else 2e-2
+    tol = {"fp32": 2e-5, "split": 5e-5}.get(prec, 2e-2)
     assert err <= tol, f"{prec}: attention max err {err}"
 
 
 @pytest.mark.parametrize("prec,variant,S", [("fp32", 0, 20), ("bf16", 0, 20), ("bf16", 1, 20), ("bf16", 2, 20),
-                                            ("bf16", 3, 20), ("bf16", 3, 300)])
+                                            ("bf16", 3, 20), ("bf16", 3, 300), ("fp32", 4, 20), ("fp32", 4, 300)])
 def test_lstm(prec, variant, S):
     """variant 0 = the resident kernel for that precision (bf16: W_hh resident in AGPR/VGPR/LDS,
     bf16 gx); variant 1 = the L2-streaming kernel in bf16 (fp32 gx); variant 2 = the resident bf16
     path with gate scales folded into W_hh and gx (the ABI scales gx), exp2-domain cell; variant 3 =
     the engine's default: W_hh split over workgroup pairs that exchange h halves every step (S = 300:
-    19 pairs, a padding pair in the last 16-block group)."""
+    19 pairs, a padding pair in the last 16-block group); fp32 variant 4 = the parity mode's default: W_hh
+    split over workgroup quads, split-bf16 products, fp32 gates / state / h (S = 300: 19 quads, padding
+    quads in the last 32-block group)."""
     N = lib()
     code, dt = PREC[prec]
     g = torch.Generator().manual_seed(3)
@@ -203,7 +207,7 @@ def test_lstm(prec, variant, S):
     ref = torch.stack(ys, 1)
     err = (out.float().cpu() - ref).abs().max().item()
     tol = 2e-5 if prec == "fp32" else 1e-2
-    assert err <= tol, f"{prec}: lstm max err {err}"
+    assert err <= tol, f"{prec}/{variant}: lstm max err {err}"
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])

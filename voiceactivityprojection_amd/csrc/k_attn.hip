@@ -396,6 +396,162 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
 
 }  // namespace
 
+
+// ------------------------------------------------------------------------------------------
+// fp32 parity-mode attention on split-bf16 operands (the default of the fp32 mode; VAP_FP32_EXACT=1
+// runs attn_kernel<float> above).  Same work split and softmax as attn_kernel (64 queries x one
+// (sequence, head), 4 waves x 16 queries, S^T = K Q^T, O^T = V^T P^T with P from registers), but
+// every fp32 operand x is carried as hi = bf16(x), lo = bf16(x - hi) and every product as
+// hi hi + hi lo + lo hi: three v_mfma_f32_16x16x32_bf16 per 16x16x32 tile-step (48 cycles) instead
+// of eight v_mfma_f32_16x16x4_f32 (256).  K and V are split once per workgroup as they are staged (K
+// as two [key][d] images, V as two transposed [d][key] images); Q once per lane; P per key tile from
+// the fp32 probabilities.  Scores live in the log2 domain (scale and slope pre-multiplied by log2 e):
+// v_exp_f32 instead of libm expf.
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int SVROW = KB * 2 + 8;  // padded V^T row (bf16): 136 B
+constexpr float LOG2E = 1.4426950408889634f;
+
+VAP_DEV void split8(const f32x4& a, const f32x4& b, chunk16& hi, chunk16& lo) {
+  const bf16x8 h = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+  const bf16x8 l = {(bf16)(a[0] - (float)h[0]), (bf16)(a[1] - (float)h[1]), (bf16)(a[2] - (float)h[2]),
+                    (bf16)(a[3] - (float)h[3]), (bf16)(b[0] - (float)h[4]), (bf16)(b[1] - (float)h[5]),
+                    (bf16)(b[2] - (float)h[6]), (bf16)(b[3] - (float)h[7])};
+  hi = __builtin_bit_cast(chunk16, h);
+  lo = __builtin_bit_cast(chunk16, l);
+}
+
+VAP_DEV f32x4 mfma3(const chunk16& ah, const chunk16& al, const chunk16& bh, const chunk16& bl, f32x4 acc) {
+  acc = mfma_chunk<bf16>(ah, bl, acc);
+  acc = mfma_chunk<bf16>(al, bh, acc);
+  return mfma_chunk<bf16>(ah, bh, acc);
+}
+
+__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char skh[KB * 128], skl[KB * 128];      // K [key][d] hi / lo
+  __shared__ __attribute__((aligned(16))) unsigned char svh[HDIM * SVROW], svl[HDIM * SVROW];  // V^T [d][key]
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qb = blockIdx.x, h = blockIdx.y, s = blockIdx.z;
+  const int ks = a.kv_swap ? (s ^ 1) : s;
+  const float* Qs = (const float*)a.Q + (int64_t)s * a.q_seq + h * HDIM;
+  const float* Ks = (const float*)a.K + (int64_t)ks * a.k_seq + h * HDIM;
+  const float* Vs = (const float*)a.V + (int64_t)ks * a.v_seq + h * HDIM;
+  const float sc = a.scale * LOG2E, sl2 = a.slopes[h] * LOG2E;
+  const int q = qb * QB + w * 16 + (lane & 15);
+  const int qc = q < a.T ? q : a.T - 1;
+
+  chunk16 qh[2], ql[2];  // d = 32kk + 8(lane>>4) .. +7 of query q
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const float* qr = Qs + (int64_t)qc * a.q_ld + kk * 32 + (lane >> 4) * 8;
+    split8(*(const f32x4*)qr, *(const f32x4*)(qr + 4), qh[kk], ql[kk]);
+  }
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb <= qb; ++kb) {
+    const int key0 = kb * KB;
+    // ---- stage K hi / lo [key][d] (8-B halves of swizzled 16-B chunks) and V^T hi / lo [d][key]
+    for (int i = tid; i < KB * 16; i += 256) {
+      const int row = i >> 4, c = i & 15;  // floats 4c .. 4c+3 of key row `row`
+      const int key = key0 + row;
+      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (key < a.T) {
+        kv = *(const f32x4*)(Ks + (int64_t)key * a.k_ld + c * 4);
+        vv = *(const f32x4*)(Vs + (int64_t)key * a.v_ld + c * 4);
+      }
+      const bf16x4 khi = {(bf16)kv[0], (bf16)kv[1], (bf16)kv[2], (bf16)kv[3]};
+      const bf16x4 klo = {(bf16)(kv[0] - (float)khi[0]), (bf16)(kv[1] - (float)khi[1]), (bf16)(kv[2] - (float)khi[2]),
+                          (bf16)(kv[3] - (float)khi[3])};
+      const int off = row * 128 + kswz2(row, c >> 1) * 16 + (c & 1) * 8;
+      *(bf16x4*)(skh + off) = khi;
+      *(bf16x4*)(skl + off) = klo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 vh = (bf16)vv[e];
+        *(bf16*)(svh + (c * 4 + e) * SVROW + row * 2) = vh;
+        *(bf16*)(svl + (c * 4 + e) * SVROW + row * 2) = (bf16)(vv[e] - (float)vh);
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T tiles: st[kt][r] = score (log2 domain) of key key0 + kt*16 + (lane>>4)*4 + r, query q
+    f32x4 st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int row = kt * 16 + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int off = row * 128 + kswz2(row, kk * 4 + (lane >> 4)) * 16;
+        acc = mfma3(*(const chunk16*)(skh + off), *(const chunk16*)(skl + off), qh[kk], ql[kk], acc);
+      }
+      st[kt] = acc;
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = key0 + kt * 16 + (lane >> 4) * 4 + r;
+        float v = st[kt][r] * sc + sl2 * (float)(key - q);
+        if (key > q) v = -INFINITY;
+        st[kt][r] = v;
+        bm = fmaxf(bm, v);
+      }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(st[kt][r] - mn);
+        st[kt][r] = p;
+        ps += p;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+
+    // ---- O^T[d][q] += V^T[d][key] P^T[key][q]; keys of k-step kk in the order of the lanes' P registers
+    chunk16 ph[2], pl[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) split8(st[2 * kk], st[2 * kk + 1], ph[kk], pl[kk]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int vr = (dt * 16 + (lane & 15)) * SVROW;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int k0 = (32 * kk + (lane >> 4) * 4) * 2, k1 = (32 * kk + 16 + (lane >> 4) * 4) * 2;
+        const u32x2 h0 = *(const u32x2*)(svh + vr + k0), h1 = *(const u32x2*)(svh + vr + k1);
+        const u32x2 l0 = *(const u32x2*)(svl + vr + k0), l1 = *(const u32x2*)(svl + vr + k1);
+        o[dt] = mfma3(chunk16{h0.x, h0.y, h1.x, h1.y}, chunk16{l0.x, l0.y, l1.x, l1.y}, ph[kk], pl[kk], o[dt]);
+      }
+    }
+    __syncthreads();
+  }
+  float lt = lsum + __shfl_xor(lsum, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  const float inv = 1.0f / lt;
+  if (q < a.T) {
+    float* orow = (float*)a.O + (int64_t)s * a.o_seq + (int64_t)q * a.o_ld + h * HDIM;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = dt * 16 + (lane >> 4) * 4;
+      store4(orow + d, o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    }
+  }
+}
+}  // namespace
+
 template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   if (a.T <= 0 || a.S <= 0 || a.H <= 0) return hipErrorInvalidValue;
@@ -408,6 +564,12 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t st) {
   }
   if (a.q0 != 0) return hipErrorInvalidValue;
   dim3 grid((a.T + QB - 1) / QB, a.H, a.S);
+  if constexpr (sizeof(T) == 4) {
+    if (a.split) {  // the fp32 parity mode's default: split-bf16 operands
+      hipLaunchKernelGGL(attn_split_kernel, grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((attn_kernel<T>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }

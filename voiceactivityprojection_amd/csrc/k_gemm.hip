@@ -18,6 +18,15 @@
 // Tile 128 x 256, 8 waves (2 along M x 4 along N, 64x64 per wave = 4x4 MFMA 16x16 tiles),
 // K staged 128 bytes per row per step (64 bf16 / 32 f32) through a double-buffered, XOR-swizzled
 // LDS image (chunk ^= (row>>1)&7 : conflict-free ds_read_b128 for 16 consecutive rows).
+//
+// gemm3_kernel (the fp32 parity mode's GEMMs, GemmArgs.split): fp32 A and W at ~fp32 accuracy on the
+// bf16 matrix cores.  Every fp32 operand x is split as x = hi + lo with hi = bf16(x), lo = bf16(x - hi)
+// (x - hi - lo ~ 2^-17 |x|), and each product as hi_a hi_w + hi_a lo_w + lo_a hi_w (the lo lo term is
+// ~2^-18 of it), three v_mfma_f32_16x16x32_bf16 with fp32 accumulation: 3 x 16 cycles per 16x16x32
+// tile-step instead of 8 x 32 for v_mfma_f32_16x16x4_f32 (5.3x the matrix rate).  W arrives pre-split
+// ([2][N][K] bf16, launch_split_bf16); A is split once per workgroup while it is staged to LDS.
+// BK = 64: A hi / lo 2 x 16 KiB + W hi / lo 2 x 32 KiB = 96 KiB, one LDS buffer (the next stage is
+// prefetched into registers during the MFMAs of this one).
 #include <cstdlib>
 
 #include "vap_common.h"
@@ -30,97 +39,11 @@ constexpr int BUF = (BM + BN) * ROWB;          // 48 KiB per stage
 
 VAP_DEV int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-template <typename T, typename TOut>
-__global__ __launch_bounds__(512) void gemm_kernel(GemmArgs g) {
-  constexpr int CE = 16 / sizeof(T);  // elements per 16-B chunk
-  constexpr int BK = 8 * CE;          // k per stage
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int M = g.M_per_seq * g.n_seq;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const T* __restrict__ A = (const T*)g.A;
-  const T* __restrict__ W = (const T*)g.W;
-
-  // ---- staging assignment: A 1024 chunks (2 / thread), B 2048 chunks (4 / thread)
-  const T* aptr[2];
-  bool aval[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = tid + i * 512, row = id >> 3, c = id & 7;
-    const int m = m0 + row;
-    aval[i] = m < M;
-    const int mm = aval[i] ? m : 0;
-    const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
-    aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * CE;
-  }
-  const T* bptr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int id = tid + i * 512, row = id >> 3, c = id & 7;
-    bptr[i] = W + (int64_t)(n0 + row) * g.K + c * CE;
-  }
-  chunk16 ra[2], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + k0) : chunk16{0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + k0);
-  };
-  auto lstore = [&](int buf) {
-    unsigned char* base = smem + buf * BUF;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + i * 512, row = id >> 3, c = id & 7;
-      *(chunk16*)(base + row * ROWB + swz(row, c) * 16) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + i * 512, row = id >> 3, c = id & 7;
-      *(chunk16*)(base + BM * ROWB + row * ROWB + swz(row, c) * 16) = rb[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = g.K / BK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-    const unsigned char* abase = smem + cur * BUF;
-    const unsigned char* bbase = abase + BM * ROWB;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      chunk16 af[4], bfr[4];
-      const int c = sub * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + (lane & 15);
-        af[i] = *(const chunk16*)(abase + row * ROWB + swz(row, c) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + (lane & 15);
-        bfr[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, c) * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
-    }
-    if (kt + 1 < nk) lstore(cur ^ 1);
-    __syncthreads();
-  }
-
-  // ---------------------------------------------------------------- epilogue
+// fused epilogue of a 128 x 256 tile (wave (wm, wn) holds acc[i][j] = 16x16 tile (rows wm*64 + 16i,
+// cols wn*64 + 16j)): bias, row norm, activation, fp32 addend, store.  smem: >= BM*4 floats, free.
+template <typename TOut>
+VAP_DEV void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][4], unsigned char* smem, int m0, int n0, int wm, int wn,
+                           int lane, int M) {
   const int colb = n0 + wn * 64 + (lane & 15);
   if (g.bias) {
 #pragma unroll
@@ -226,6 +149,226 @@ __global__ __launch_bounds__(512) void gemm_kernel(GemmArgs g) {
     }
 }
 
+template <typename T, typename TOut>
+__global__ __launch_bounds__(512) void gemm_kernel(GemmArgs g) {
+  constexpr int CE = 16 / sizeof(T);  // elements per 16-B chunk
+  constexpr int BK = 8 * CE;          // k per stage
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int M = g.M_per_seq * g.n_seq;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const T* __restrict__ A = (const T*)g.A;
+  const T* __restrict__ W = (const T*)g.W;
+
+  // ---- staging assignment: A 1024 chunks (2 / thread), B 2048 chunks (4 / thread)
+  const T* aptr[2];
+  bool aval[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    const int m = m0 + row;
+    aval[i] = m < M;
+    const int mm = aval[i] ? m : 0;
+    const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
+    aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * CE;
+  }
+  const T* bptr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    bptr[i] = W + (int64_t)(n0 + row) * g.K + c * CE;
+  }
+  chunk16 ra[2], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + k0) : chunk16{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + k0);
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      *(chunk16*)(base + row * ROWB + swz(row, c) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      *(chunk16*)(base + BM * ROWB + row * ROWB + swz(row, c) * 16) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+    const unsigned char* abase = smem + cur * BUF;
+    const unsigned char* bbase = abase + BM * ROWB;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      chunk16 af[4], bfr[4];
+      const int c = sub * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + (lane & 15);
+        af[i] = *(const chunk16*)(abase + row * ROWB + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + (lane & 15);
+        bfr[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  gemm_epilogue<TOut>(g, acc, smem, m0, n0, wm, wn, lane, M);
+}
+
+
+// fp32 A x split W on the bf16 matrix cores (see the header): C = epi(A . W^T) at ~fp32 accuracy.
+// Staging per 64-k stage: thread t loads 4 A chunks (4 floats: row id >> 4, k 4 (id & 15)) and 4 + 4
+// W chunks (8 bf16 of the hi / lo images: row id >> 3, k 8 (id & 7)); A is split while it is stored.
+constexpr int G3_AIMG = BM * ROWB, G3_WIMG = BN * ROWB;                      // 16 KiB, 32 KiB
+constexpr int G3_LDS = 2 * G3_AIMG + 2 * G3_WIMG;                            // 96 KiB
+__global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G3_LDS];
+  unsigned char* Ahi = smem;
+  unsigned char* Alo = smem + G3_AIMG;
+  unsigned char* Whi = smem + 2 * G3_AIMG;
+  unsigned char* Wlo = Whi + G3_WIMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int M = g.M_per_seq * g.n_seq;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const float* __restrict__ A = (const float*)g.A;
+  const bf16* __restrict__ Wh = (const bf16*)g.W;
+  const bf16* __restrict__ Wl = Wh + (int64_t)g.N * g.K;
+
+  const float* aptr[4];
+  bool aval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + i * 512, row = id >> 4, c = id & 15;
+    const int m = m0 + row;
+    aval[i] = m < M;
+    const int mm = aval[i] ? m : 0;
+    const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
+    aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * 4;
+  }
+  int64_t woff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
+    woff[i] = (int64_t)(n0 + row) * g.K + c * 8;
+  }
+  chunk16 ra[4], rh[4], rl[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + k0) : chunk16{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rh[i] = *(const chunk16*)(Wh + woff[i] + k0);
+      rl[i] = *(const chunk16*)(Wl + woff[i] + k0);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 512, row = id >> 4, c = id & 15;  // floats 4c .. 4c+3 = bf16 bytes 8c .. 8c+7
+      const f32x4 v = __builtin_bit_cast(f32x4, ra[i]);
+      const bf16x4 hi = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      const bf16x4 lo = {(bf16)(v[0] - (float)hi[0]), (bf16)(v[1] - (float)hi[1]), (bf16)(v[2] - (float)hi[2]),
+                         (bf16)(v[3] - (float)hi[3])};
+      const int off = row * ROWB + swz(row, c >> 1) * 16 + (c & 1) * 8;
+      *(bf16x4*)(Ahi + off) = hi;
+      *(bf16x4*)(Alo + off) = lo;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;
+      const int off = row * ROWB + swz(row, c) * 16;
+      *(chunk16*)(Whi + off) = rh[i];
+      *(chunk16*)(Wlo + off) = rl[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / 64;
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * 64);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      chunk16 ah[4], al[4], bh[4], bl[4];
+      const int c = sub * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + (lane & 15);
+        const int off = row * ROWB + swz(row, c) * 16;
+        ah[i] = *(const chunk16*)(Ahi + off);
+        al[i] = *(const chunk16*)(Alo + off);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + (lane & 15);
+        const int off = row * ROWB + swz(row, c) * 16;
+        bh[j] = *(const chunk16*)(Whi + off);
+        bl[j] = *(const chunk16*)(Wlo + off);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = mfma_chunk<bf16>(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma_chunk<bf16>(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma_chunk<bf16>(ah[i], bh[j], acc[i][j]);
+        }
+    }
+    __syncthreads();  // every wave is done reading this stage
+    if (kt + 1 < nk) {
+      lstore();
+      __syncthreads();
+    }
+  }
+  gemm_epilogue<float>(g, acc, smem, m0, n0, wm, wn, lane, M);
+}
+
+// fp32 [n] -> bf16 hi [0, n) and lo [n, 2n): x = hi + lo + O(2^-17 |x|)
+__global__ void split_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float x = in[i];
+    const bf16 hi = (bf16)x;
+    out[i] = hi;
+    out[n + i] = (bf16)(x - (float)hi);
+  }
+}
+
 }  // namespace
 
 template <typename T, typename TOut>
@@ -242,7 +385,20 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (aligned && !g.small_tiles) return launch_gemm2<TOut>(g, st);
   }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
+  if constexpr (sizeof(T) == 4 && sizeof(TOut) == 4) {
+    if (g.split) {  // fp32 operands through the split-bf16 kernel (W: [2][N][K] bf16 from launch_split_bf16)
+      if (g.K % 64 != 0) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(gemm3_kernel, grid, dim3(512), 0, st, g);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_kernel<T, TOut>), grid, dim3(512), 0, st, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(256), dim3(256), 0, st, in, out, n);
   return hipGetLastError();
 }
 

@@ -737,6 +737,214 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// fp32 parity mode: W_hh split over a QUAD of workgroups, products on split-bf16 operands.
+//
+// The fp32 recurrence on v_mfma_f32_16x16x4_f32 (lstm_kernel<float>) streams W_hh from L2 at one CU
+// per 16 sequences: 1024 MFMAs of 32 cycles per wave and step (~13.6 us of issue, 19 us per step).
+// Here both operands are fp32 values carried as hi + lo bf16 pairs (hi = bf16(x), lo = bf16(x - hi))
+// and every product as hi_w hi_h + hi_w lo_h + lo_w hi_h, three v_mfma_f32_16x16x32_bf16 with fp32
+// accumulation (the lo lo term is ~2^-18 of the product; the gate pre-activations stay within ~1e-6 of
+// fp32).  Workgroup q of a quad owns hidden units [64q, 64q + 64): 4 gates x 64 units = 256 W_hh rows,
+// hi + lo = 256 KiB, held in registers by 4 waves (one per SIMD, 64 fragments = 256 VGPRs each); wave w
+// owns units 64q + 16w .. +16 (one row tile per gate: 96 MFMAs and 4 cells per lane per step, ~1.5k
+// cycles of matrix issue).  The cell update runs in fp32 (v_exp / v_rcp forms, abs. error ~2e-7, as
+// lstm_kernel<float>); c and h stay fp32 and h_t rows are stored fp32.
+// Exchange (as lstm_pair_kernel, with three partners): every lane publishes its 4 fp32 h values as four
+// 8-byte {h, tag} granules in two 16-byte write-through stores into the quad's slot for step parity t&1;
+// the same lane of each partner polls those slots (sc1 loads) until every tag matches, then writes the
+// values, split into hi / lo, into its two LDS images of h.  The polls are issued before the own-unit
+// k-steps (2 of 8), so their latency overlaps those MFMAs.  Two parity slots suffice (a quarter writes
+// h_t only after reading every partner's h_{t-1}, published after they read our h_{t-2}).  Quads are
+// blocks (b, b+8, b+16, b+24) of each 32-block group (one XCD under round-robin placement: speed only);
+// every spin is bounded (~2 s, then the error word is set and the launch runs on without waiting).
+// ------------------------------------------------------------------------------------------
+constexpr int Q_NW = 4, Q_NF = 64;              // waves per workgroup, fragments per wave (4 g x 8 kk x hi/lo)
+constexpr int Q_SLOT = 4 * 2 * 256 * 2;         // 16-byte exchange slots per quad: [quarter][parity][tid][2]
+
+template <int Q>
+VAP_DEV void quad_steps(const float* __restrict__ gxs, int Tn, int S, const chunk16 (&wf)[Q_NF], unsigned char* hh,
+                        unsigned char* hl, __amdgpu_buffer_rsrc_t xr, __amdgpu_buffer_rsrc_t orsc, uint32_t o_lane,
+                        uint32_t tag_base, unsigned* err, int tid) {
+  const int lane = tid & 63, w = tid >> 6, sl = lane & 15;
+  const int u0 = 64 * Q + 16 * w + 4 * (lane >> 4);
+  auto hfrag = [&](const unsigned char* img, int kk) -> chunk16 {  // h[32kk + 8(lane>>4) + e][seq sl]
+    return *(const chunk16*)(img + sl * 512 + (((kk * 4 + (lane >> 4)) ^ sl) << 4));
+  };
+  auto hput = [&](int u, float a, float b, float c, float d) {  // units u .. u+3 of sequence sl, split
+    const bf16x4 hi = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+    const bf16x4 lo = {(bf16)(a - (float)hi[0]), (bf16)(b - (float)hi[1]), (bf16)(c - (float)hi[2]),
+                       (bf16)(d - (float)hi[3])};
+    const int off = sl * 512 + (((u >> 3) ^ sl) << 4) + (u & 7) * 2;
+    *(bf16x4*)(hh + off) = hi;
+    *(bf16x4*)(hl + off) = lo;
+  };
+  // exchange slot byte offsets: quarter qq, parity par, this thread, granule pair j
+  auto xoff = [&](int qq, int par, int j) -> uint32_t { return (uint32_t)((((qq * 2 + par) * 256 + tid) * 2 + j) * 16); };
+  // gates of step t: 4 x 16 B (gate g at column g*256 + u0), two steps ahead (compiler-tracked loads: the
+  // waits are the compiler's, so no register of an in-flight load is ever read early)
+  auto gload = [&](u32x4 (&gv)[4], int t) {
+    const float* a = gxs + (int64_t)t * 1024;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gv[g] = *(const u32x4*)(a + g * 256);
+  };
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  u32x4 ga[4], gb[4];
+  gload(ga, 0);
+  gload(gb, Tn > 1 ? 1 : 0);
+  bool dead = false;
+  // the weight fragments stay in AGPRs as the MFMAs' A operand (inline asm, mfma_a): LEAD pads the
+  // VALU-write -> srcC wait of a fresh accumulator, TAIL the MFMA -> VALU wait after the step's last one
+  constexpr int KLAST = Q == 3 ? 5 : 7;
+  auto kstep = [&](f32x4 (&acc)[4], auto kkc) {
+    constexpr int kk = decltype(kkc)::value;
+    constexpr int LEAD = kk == 2 * Q ? 1 : 0, TAIL = kk == KLAST ? 1 : 0;
+    const chunk16 bh = hfrag(hh, kk), bl = hfrag(hl, kk);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mfma_a<LEAD, 0>(acc[g], wf[(g * 8 + kk) * 2 + 1], bh);  // lo_w hi_h
+#pragma unroll
+    for (int g = 0; g < 4; ++g) mfma_a<0, 0>(acc[g], wf[(g * 8 + kk) * 2], bl);        // hi_w lo_h
+    mfma_a<0, 0>(acc[0], wf[(0 * 8 + kk) * 2], bh);                                      // hi_w hi_h
+    mfma_a<0, 0>(acc[1], wf[(1 * 8 + kk) * 2], bh);
+    mfma_a<0, 0>(acc[2], wf[(2 * 8 + kk) * 2], bh);
+    mfma_a<0, TAIL>(acc[3], wf[(3 * 8 + kk) * 2], bh);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  using I6 = std::integral_constant<int, 6>;
+  using I7 = std::integral_constant<int, 7>;
+  auto step = [&](const int t, u32x4 (&gc)[4]) {
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = __builtin_bit_cast(f32x4, gc[g]);
+    u32x4 xv[3][2];
+    const int par = (t - 1) & 1;
+    if (t > 0) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) xv[p][j] = xload(xr, xoff((Q + 1 + p) & 3, par, j));
+    }
+    gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);  // gates of step t+2 into the slot just consumed
+    kstep(acc, std::integral_constant<int, 2 * Q>{});
+    kstep(acc, std::integral_constant<int, 2 * Q + 1>{});
+    if (t > 0) {
+      __builtin_amdgcn_sched_barrier(0);  // the own-unit MFMAs stay ahead of the wait
+      const uint32_t want = tag_base + (uint32_t)(t - 1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        uint64_t t0 = 0;
+        while (!dead && !__all(xv[p][0][1] == want && xv[p][0][3] == want && xv[p][1][1] == want && xv[p][1][3] == want)) {
+          if (!t0) {
+            t0 = __builtin_amdgcn_s_memrealtime();
+          } else if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            if (err && lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            dead = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          xv[p][0] = xload(xr, xoff((Q + 1 + p) & 3, par, 0));
+          xv[p][1] = xload(xr, xoff((Q + 1 + p) & 3, par, 1));
+        }
+        const int uq = 64 * ((Q + 1 + p) & 3) + 16 * w + 4 * (lane >> 4);  // the partner lane's units
+        hput(uq, __builtin_bit_cast(float, xv[p][0][0]), __builtin_bit_cast(float, xv[p][0][2]),
+             __builtin_bit_cast(float, xv[p][1][0]), __builtin_bit_cast(float, xv[p][1][2]));
+      }
+    }
+    // (barriers as asm with a memory clobber: the s_barrier builtin does not order the LDS reads after it)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B1: the partners' units of h_{t-1} are in
+                                                                     // the images
+    if constexpr (Q != 0) { kstep(acc, I0{}); kstep(acc, I1{}); }
+    if constexpr (Q != 1) { kstep(acc, I2{}); kstep(acc, I3{}); }
+    if constexpr (Q != 2) { kstep(acc, I4{}); kstep(acc, I5{}); }
+    if constexpr (Q != 3) { kstep(acc, I6{}); kstep(acc, I7{}); }
+    __builtin_amdgcn_sched_barrier(0);  // the cell's VALU reads stay behind the TAIL wait
+    float hv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ig = cell_sig(acc[0][r]), fg = cell_sig(acc[1][r]), gg = cell_tanh(acc[2][r]), og = cell_sig(acc[3][r]);
+      c[r] = fg * c[r] + ig * gg;
+      hv[r] = og * cell_tanh(c[r]);
+    }
+    const uint32_t tag = tag_base + (uint32_t)t;
+    const u32x4 x0 = {__builtin_bit_cast(uint32_t, hv[0]), tag, __builtin_bit_cast(uint32_t, hv[1]), tag};
+    const u32x4 x1 = {__builtin_bit_cast(uint32_t, hv[2]), tag, __builtin_bit_cast(uint32_t, hv[3]), tag};
+    const u32x4 hrow = {__builtin_bit_cast(uint32_t, hv[0]), __builtin_bit_cast(uint32_t, hv[1]),
+                        __builtin_bit_cast(uint32_t, hv[2]), __builtin_bit_cast(uint32_t, hv[3])};
+    buf_store16_wt(xr, xoff(Q, t & 1, 0), x0);  // write-through (sc1): the partners poll with sc1 loads
+    buf_store16_wt(xr, xoff(Q, t & 1, 1), x1);
+    buf_store16(orsc, o_lane + (uint32_t)t * (HD * 4), hrow);
+    hput(u0, hv[0], hv[1], hv[2], hv[3]);  // own units of h_t (this step's own-unit reads retired before B1)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B2: own h_t visible to every wave
+  };
+  for (int t = 0; t < Tn; t += 2) {
+    step(t, ga);
+    if (t + 1 < Tn) step(t + 1, gb);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void lstm_quad_kernel(const float* __restrict__ gx, int S, int Tn,
+                                                           const chunk16* __restrict__ wp, float* __restrict__ out,
+                                                           int64_t out_seq_stride, u32x4* xbuf, unsigned xtag,
+                                                           unsigned* err) {
+  __shared__ __attribute__((aligned(16))) unsigned char hh[NS * 512];  // h_{t-1} hi [seq][256] bf16, chunk ^= seq
+  __shared__ __attribute__((aligned(16))) unsigned char hl[NS * 512];  // h_{t-1} lo
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int grp = (b >> 5) * 8 + (b & 7), q = (b >> 3) & 3;
+  if (grp * NS >= S) return;  // padding quad (all four quarters leave)
+  const int sl = lane & 15;
+  const int seq = grp * NS + sl;
+  const bool valid = seq < S;
+  const int u0 = 64 * q + 16 * w + 4 * (lane >> 4);
+
+  chunk16 wf[Q_NF];  // fragment (g*8 + kk)*2 + s: rows g*256 + 64q + 16w + (lane&15), k = 32kk + 8(lane>>4) + e
+  const chunk16* wsrc = wp + (int64_t)(q * Q_NW + w) * Q_NF * 64 + lane;
+#pragma unroll
+  for (int f = 0; f < Q_NF; ++f) wf[f] = wsrc[f * 64];
+  for (int i = tid; i < NS * 512 / 4; i += 256) {
+    ((unsigned*)hh)[i] = 0u;  // h_{-1} = 0
+    ((unsigned*)hl)[i] = 0u;
+  }
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xbuf + (int64_t)grp * Q_SLOT, (uint32_t)(Q_SLOT * 16));
+  const __amdgpu_buffer_rsrc_t orsc =
+      make_rsrc(out + (int64_t)grp * NS * out_seq_stride, (uint32_t)((int64_t)min(NS, S - grp * NS) * out_seq_stride * 4));
+  const uint32_t o_lane = (uint32_t)(((int64_t)sl * out_seq_stride + u0) * 4);  // missing sequences: out of range
+  const float* gxs = gx + (int64_t)(valid ? seq : grp * NS) * Tn * 1024 + u0;
+  __syncthreads();
+  const uint32_t tag_base = xtag;  // tag of step t: xtag + t
+  switch (q) {
+    case 0: quad_steps<0>(gxs, Tn, S, wf, hh, hl, xr, orsc, o_lane, tag_base, err, tid); break;
+    case 1: quad_steps<1>(gxs, Tn, S, wf, hh, hl, xr, orsc, o_lane, tag_base, err, tid); break;
+    case 2: quad_steps<2>(gxs, Tn, S, wf, hh, hl, xr, orsc, o_lane, tag_base, err, tid); break;
+    default: quad_steps<3>(gxs, Tn, S, wf, hh, hl, xr, orsc, o_lane, tag_base, err, tid); break;
+  }
+}
+
+// quad layout: Wq[q][w][f = (g*8 + kk)*2 + s][lane][e] = split_s(W[g*256 + 64q + 16w + (l&15)][32kk + 8(l>>4) + e])
+__global__ void pack_whh_quad_kernel(const float* __restrict__ whh, bf16* __restrict__ out) {
+  const int64_t n = (int64_t)G4 * HD * 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7);
+    const int l = (int)((i >> 3) & 63);
+    const int f = (int)((i >> 9) & 63);
+    const int w = (int)((i >> 15) & 3);
+    const int q = (int)(i >> 17);
+    const int sp = f & 1, kk = (f >> 1) & 7, g = f >> 4;
+    const int row = g * HD + 64 * q + 16 * w + (l & 15);
+    const int k = 32 * kk + 8 * (l >> 4) + e;
+    const float x = whh[(int64_t)row * HD + k];
+    const bf16 hi = (bf16)x;
+    out[i] = sp ? (bf16)(x - (float)hi) : hi;
+  }
+}
+
 // Wp[w][f = rt*8 + kg][lane][e] = W[g*256 + 64w + 16ut + (l&15)][32kg + 8(l>>4) + e],  rt = g*4 + ut
 // gate-row scale of the pre-scaled packing (lstm_cell<true>): -log2e on i / f / o, 2 log2e on g
 VAP_DEV float gate_scale(int row) { return (row >> 8) == 2 ? KC : -0.5f * KC; }
@@ -882,6 +1090,23 @@ hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16*
   else
     hipLaunchKernelGGL((lstm_pair_kernel<true, false>), grid, dim3(512), 0, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
                        out_seq_stride, sy, (u32x4*)xbuf);
+  return hipGetLastError();
+}
+size_t lstm_quad_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * Q_SLOT * 16; }
+
+hipError_t launch_lstm_quad(const float* gx, int S, int Tn, const bf16* whh_quad, float* out, int64_t out_seq_stride,
+                            hipStream_t st, void* xbuf, unsigned xtag, unsigned* err) {
+  if (S <= 0 || Tn <= 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+  // the per-lane buffer offsets of the output rows are 32-bit
+  if ((int64_t)min(NS, S) * out_seq_stride * 4 >= 0x7FFFFFF0LL || (int64_t)Tn * HD > out_seq_stride) return hipErrorInvalidValue;
+  const int groups = (S + NS - 1) / NS;
+  const dim3 grid(32 * ((groups + 7) / 8));  // quads (b, b+8, b+16, b+24) of every 32 blocks; padding quads exit
+  hipLaunchKernelGGL(lstm_quad_kernel, grid, dim3(256), 0, st, gx, S, Tn, (const chunk16*)whh_quad, out, out_seq_stride,
+                     (u32x4*)xbuf, xtag, err);
+  return hipGetLastError();
+}
+hipError_t launch_pack_whh_quad(const float* whh, bf16* packed, hipStream_t st) {
+  hipLaunchKernelGGL(pack_whh_quad_kernel, dim3(256), dim3(256), 0, st, whh, packed);
   return hipGetLastError();
 }
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st) {

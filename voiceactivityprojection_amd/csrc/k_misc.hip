@@ -10,76 +10,63 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // conv0 (1 -> 256, k=10, s=5, p=3) -> ChannelNorm (unbiased var over 256 ch, eps 1e-5) -> ReLU
 // reference: vap/encoder_components.py:83-84 (conv0/batchNorm0), :62-70 (ChannelNorm), :99.
-// Block = 64 positions of one sequence (seq = 2*clip + channel); 4 threads per position, 64 channels each (registers),
-// row stats by two 4-lane butterflies.  Output time-major [seq][2 + L0 + 2][256] (2 pad rows
-// each side = conv1's zero padding).
+// (fp32 parity mode; the bf16 mode fuses conv0 into conv1, k_conv01.hip.)  Store-bound: the
+// output is 1 KiB per position (fp32), 131 MB per 20 s stereo clip.  Block = 64 positions of one
+// sequence (seq = 2*clip + channel); lane l owns channels 4l .. 4l+3 (its 40 weights in registers),
+// wave w positions 16w .. 16w+15: every output row leaves as ONE 1 KiB store instruction (16 B per
+// lane, fully coalesced), the row statistics by wave reductions.  The 326 samples of the block are
+// staged in LDS and read as broadcasts.  Output time-major [seq][2 + L0 + 2][256] (2 pad rows each
+// side = conv1's zero padding).
 // ------------------------------------------------------------------------------------------
-constexpr int C0 = 256, KW0 = 10, WROW = 260;  // padded LDS row (bank spread across quarters)
+constexpr int C0 = 256, KW0 = 10, P0 = 64, NSMP = P0 * 5 + 6;
 
 template <typename T>
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ wav, int B, int64_t N, int L0,
                                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                                    const float* __restrict__ gam, const float* __restrict__ bet,
                                                    T* __restrict__ out, int64_t out_seq_stride) {
-  __shared__ float sw[KW0 * WROW];
-  __shared__ float sb[3 * WROW];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < C0 * KW0; i += 256) {
-    const int c = i / KW0, k = i - c * KW0;
-    sw[k * WROW + c + (c >> 6)] = w0[i];
+  __shared__ float smp[NSMP + 2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int s = blockIdx.y;  // sequence = 2 * clip + channel (clip-major == the [B][2][N] waveform)
+  const int p0 = blockIdx.x * P0;
+  const float* src = wav + (int64_t)s * N;
+  const int64_t i0 = (int64_t)p0 * 5 - 3;
+  for (int i = tid; i < NSMP; i += 256) {
+    const int64_t j = i0 + i;
+    smp[i] = (j >= 0 && j < N) ? src[j] : 0.f;
   }
-  {
-    const int c = tid;
-    sb[0 * WROW + c + (c >> 6)] = b0[c];
-    sb[1 * WROW + c + (c >> 6)] = gam[c];
-    sb[2 * WROW + c + (c >> 6)] = bet[c];
+  float wv[4][KW0], bv[4], gv[4], be[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = 4 * lane + e;
+#pragma unroll
+    for (int k = 0; k < KW0; ++k) wv[e][k] = w0[c * KW0 + k];
+    bv[e] = b0[c];
+    gv[e] = gam[c];
+    be[e] = bet[c];
   }
   __syncthreads();
-  const int s = blockIdx.y;  // sequence = 2 * clip + channel (clip-major == the [B][2][N] waveform)
-  const int pos = blockIdx.x * 64 + (tid >> 2);
-  const int q = tid & 3;
-  if (pos >= L0) return;  // whole 4-lane groups exit together (shuffles stay within groups)
-  const float* src = wav + (int64_t)s * N;
-  float smp[KW0];
-  const int64_t i0 = (int64_t)pos * 5 - 3;
-#pragma unroll
-  for (int k = 0; k < KW0; ++k) {
-    const int64_t i = i0 + k;
-    smp[k] = (i >= 0 && i < N) ? src[i] : 0.f;
-  }
-  float x[64];
-  float sum = 0.f;
-  const int cb = q * 64 + q;  // LDS column base incl. pad
-#pragma unroll
-  for (int cc = 0; cc < 64; ++cc) {
-    float v = sb[cb + cc];
-#pragma unroll
-    for (int k = 0; k < KW0; ++k) v = fmaf(sw[k * WROW + cb + cc], smp[k], v);
-    x[cc] = v;
-    sum += v;
-  }
-  sum += __shfl_xor(sum, 1, 64);
-  sum += __shfl_xor(sum, 2, 64);
-  const float mean = sum * (1.0f / C0);
-  float ss = 0.f;
-#pragma unroll
-  for (int cc = 0; cc < 64; ++cc) {
-    const float d = x[cc] - mean;
-    ss += d * d;
-  }
-  ss += __shfl_xor(ss, 1, 64);
-  ss += __shfl_xor(ss, 2, 64);
-  const float rstd = rsqrtf(ss * (1.0f / (C0 - 1)) + 1e-5f);
-  T* o = out + (int64_t)s * out_seq_stride + (int64_t)(pos + 2) * C0 + q * 64;
-#pragma unroll
-  for (int cc = 0; cc < 64; cc += 4) {
-    float y[4];
+#pragma unroll 2
+  for (int j = 0; j < 16; ++j) {
+    const int pl = w * 16 + j, pos = p0 + pl;
+    if (pos >= L0) break;  // wave-uniform
+    float x[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float v = (x[cc + e] - mean) * rstd * sb[WROW + cb + cc + e] + sb[2 * WROW + cb + cc + e];
-      y[e] = fmaxf(v, 0.f);
+      float v = bv[e];
+#pragma unroll
+      for (int k = 0; k < KW0; ++k) v = fmaf(wv[e][k], smp[pl * 5 + k], v);
+      x[e] = v;
     }
-    store4(o + cc, y[0], y[1], y[2], y[3]);
+    const float mean = wave_sum((x[0] + x[1]) + (x[2] + x[3])) * (1.0f / C0);
+    float ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ss = fmaf(x[e] - mean, x[e] - mean, ss);
+    const float rstd = rsqrtf(wave_sum(ss) * (1.0f / (C0 - 1)) + 1e-5f);
+    float y[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = fmaxf((x[e] - mean) * rstd * gv[e] + be[e], 0.f);
+    store4(out + (int64_t)s * out_seq_stride + (int64_t)(pos + 2) * C0 + 4 * lane, y[0], y[1], y[2], y[3]);
   }
 }
 

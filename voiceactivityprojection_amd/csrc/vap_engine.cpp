@@ -103,6 +103,12 @@ struct vap_handle {
   int test_drop_ready = -1;  // tests only (vap_test_drop_ready): never publish ready[c] -> the wait times out
   int lstm_xplain = 0;       // VAP_LSTM_XPLAIN / vap_test_lstm_xplain: pair-exchange store policy (0 = by handshake)
   int lstm_max_wg = 0;  // VAP_LSTM_MAX_WG: persistent recurrence launches at most this many workgroups
+  // fp32 parity mode: GEMMs on split-bf16 operands (k_gemm.hip gemm3_kernel; VAP_FP32_EXACT=1: the exact
+  // fp32-MFMA kernels); fp32 packed weight -> its split copy [2][N][K] bf16
+  bool fp32_split = true;
+  bool fp32_quad = false;  // VAP_FP32_QUAD=1: the recurrence on the quad-split kernel (k_lstm.hip lstm_quad_kernel)
+  std::map<const void*, const void*> split_of;
+  std::map<std::string, int64_t> packed_numel;
   unsigned epoch = 0;
   unsigned done_expect[MAXMB] = {};
   bool wait_value = false;  // device supports hipStreamWaitValue32 / hipStreamWriteValue32
@@ -369,6 +375,15 @@ hipError_t gemm(const GemmArgs& g, hipStream_t st, bool out_f32) {
   return launch_gemm<float, float>(g, st);
 }
 
+}  // namespace
+
+// fp32 mode: the GEMMs take the split-bf16 copy of their weight (three bf16 MFMAs per tile-step at ~fp32
+// accuracy, k_gemm.hip gemm3_kernel) unless the handle runs the exact fp32-MFMA kernels (VAP_FP32_EXACT=1)
+template <typename T>
+hipError_t hgemm(const vap_handle* h, GemmArgs g, hipStream_t st, bool out_f32);
+
+namespace {
+
 GemmArgs gargs(const void* A, int64_t lda, int64_t aseq, const void* W, int K, int N, const float* bias, int Mps, int nseq,
                void* C, int64_t ldc, int64_t cseq) {
   GemmArgs g{};
@@ -471,6 +486,7 @@ int pack_all(vap_handle* h, hipStream_t st) {
     void* p = nullptr;
     if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
     h->packed[name] = p;
+    h->packed_numel[name] = n;
     return (T*)p;
   };
   const std::string g = "encoder.encoder.gEncoder";
@@ -510,6 +526,10 @@ int pack_all(vap_handle* h, hipStream_t st) {
       HIPCHK(launch_convert<T>(h->P(p + "weight_ih" + s), wih, 4 * D * D, st));
       HIPCHK(launch_pack_whh<T>(h->P(p + "weight_hh" + s), whh, st));
       HIPCHK(launch_add_vec(h->P(p + "bias_ih" + s), h->P(p + "bias_hh" + s), b, 4 * D, st));
+      void* wq = nullptr;  // the quad-split recurrence's split-bf16 W_hh (k_lstm.hip lstm_quad_kernel)
+      if (hipMalloc(&wq, (size_t)2 * 4 * D * D * sizeof(bf16)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc lstm");
+      h->packed["whhq" + s] = wq;
+      HIPCHK(launch_pack_whh_quad(h->P(p + "weight_hh" + s), (bf16*)wq, st));
     }
   }
   {
@@ -575,8 +595,38 @@ int pack_all(vap_handle* h, hipStream_t st) {
   }
   if ((rc = cat("head", {"vap_head.weight"}))) return rc;
   if (!h->dims.mono && (rc = rp_copy("head", 256))) return rc;
+  if constexpr (sizeof(T) == 4) {  // split-bf16 copies of every GEMM weight (not W_hh: the recurrence packs its own)
+    std::vector<std::pair<std::string, int64_t>> todo;
+    for (auto& kv : h->packed_numel)
+      if (kv.first.rfind("whh", 0) != 0) todo.push_back(kv);
+    for (auto& kv : todo) {
+      void* sp = nullptr;
+      if (hipMalloc(&sp, kv.second * 2 * sizeof(bf16)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc split weight");
+      h->packed[kv.first + "@s"] = sp;
+      HIPCHK(launch_split_bf16((const float*)h->packed.at(kv.first), (bf16*)sp, kv.second, st));
+      h->split_of[h->packed.at(kv.first)] = sp;
+    }
+  }
   return VAP_OK;
 }
+
+}  // namespace
+
+template <typename T>
+hipError_t hgemm(const vap_handle* h, GemmArgs g, hipStream_t st, bool out_f32) {
+  if constexpr (sizeof(T) == 4) {
+    if (h->fp32_split) {
+      auto it = h->split_of.find(g.W);
+      if (it != h->split_of.end()) {
+        g.W = it->second;
+        g.split = 1;
+      }
+    }
+  }
+  return gemm<T>(g, st, out_f32);
+}
+
+namespace {
 
 // ------------------------------------------------------------------------ forward
 // Sequences are CLIP-MAJOR: seq s = 2*clip + channel (speaker), matching the [B][2][N] waveform,
@@ -695,20 +745,21 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(gemm<T>(gargs(LN, D, t1, h->W<T>(pre + ".qkv"), D, 3 * D, nullptr, T_, S, QKV, 3 * D, t3), st, false));
+    HIPCHK(hgemm<T>(h, gargs(LN, D, t1, h->W<T>(pre + ".qkv"), D, 3 * D, nullptr, T_, S, QKV, 3 * D, t3), st, false));
     if (cross)  // K/V of the cross attention come from the UN-normalised pre-layer x (modules.py:265-272)
-      HIPCHK(gemm<T>(gargs(RAW, D, t1, h->W<T>(pre + ".kvc"), D, 2 * D, nullptr, T_, S, KVC, 2 * D, t2), st, false));
+      HIPCHK(hgemm<T>(h, gargs(RAW, D, t1, h->W<T>(pre + ".kvc"), D, 2 * D, nullptr, T_, S, KVC, 2 * D, t2), st, false));
   }
   {
     Timed tm(h, VAP_K_ATTN, st);
     AttnArgs a{QKV, 3 * D, t3, QKV + D, 3 * D, t3, QKV + 2 * D, 3 * D, t3, ATT, D, t1, h->P(pre + ".mha.m"), S, T_, H,
                0, scale};
+    a.split = h->fp32_split ? 1 : 0;
     HIPCHK(launch_attention<T>(a, st));
     if (int rc = attn_maps<T>(h, a, cross ? 2 : 0, layer, r, st)) return rc;
   }
   {
     Timed tm(h, VAP_K_TR_GEMM, st);
-    HIPCHK(gemm<T>(resid(gargs(ATT, D, t1, h->W<T>(pre + ".o"), D, D, nullptr, T_, S, X, D, t1)), st, true));
+    HIPCHK(hgemm<T>(h, resid(gargs(ATT, D, t1, h->W<T>(pre + ".o"), D, D, nullptr, T_, S, X, D, t1)), st, true));
   }
   if (cross) {
     {
@@ -718,18 +769,19 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(gemm<T>(gargs(LN, D, t1, h->W<T>(pre + ".qc"), D, D, nullptr, T_, S, QC, D, t1), st, false));
+      HIPCHK(hgemm<T>(h, gargs(LN, D, t1, h->W<T>(pre + ".qc"), D, D, nullptr, T_, S, QC, D, t1), st, false));
     }
     {
       Timed tm(h, VAP_K_ATTN, st);
       AttnArgs a{QC, D, t1, KVC, 2 * D, t2, KVC + D, 2 * D, t2, ATT, D, t1, h->P(pre + ".mha_cross.m"), S, T_, H, 1,
                  scale};
+      a.split = h->fp32_split ? 1 : 0;
       HIPCHK(launch_attention<T>(a, st));
       if (int rc = attn_maps<T>(h, a, 1, layer, r, st)) return rc;
     }
     {
       Timed tm(h, VAP_K_TR_GEMM, st);
-      HIPCHK(gemm<T>(resid(gargs(ATT, D, t1, h->W<T>(pre + ".oc"), D, D, nullptr, T_, S, X, D, t1)), st, true));
+      HIPCHK(hgemm<T>(h, resid(gargs(ATT, D, t1, h->W<T>(pre + ".oc"), D, D, nullptr, T_, S, X, D, t1)), st, true));
     }
   }
   {
@@ -741,8 +793,8 @@ int tr_layer(vap_handle* h, const Plan& p, unsigned char* ws, const std::string&
     Timed tm(h, VAP_K_TR_GEMM, st);
     GemmArgs g = gargs(LN, D, t1, h->W<T>(pre + ".w1"), D, 3 * D, nullptr, T_, S, FF, 3 * D, t3);
     g.act = 2;
-    HIPCHK(gemm<T>(g, st, false));
-    HIPCHK(gemm<T>(resid(gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1)), st, true));
+    HIPCHK(hgemm<T>(h, g, st, false));
+    HIPCHK(hgemm<T>(h, resid(gargs(FF, 3 * D, t3, h->W<T>(pre + ".w2"), 3 * D, D, nullptr, T_, S, X, D, t1)), st, true));
   }
   return VAP_OK;
 }
@@ -796,13 +848,15 @@ int front_end(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     ga.act = 1;
     ga.gamma = h->P(g + ".batchNorm" + c + ".weight");
     ga.beta = h->P(g + ".batchNorm" + c + ".bias");
-    HIPCHK(gemm<T>(ga, st, false));
+    HIPCHK(hgemm<T>(h, ga, st, false));
   }
   return VAP_OK;
 }
 
 int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer, bf16* out, int64_t out_stride,
                hipStream_t st, const LstmSync* sy, int xg0);
+int launch_rec_f32(vap_handle* h, const float* GX, int S, int L4, int layer, float* out, int64_t out_stride,
+                   hipStream_t st, int xg0);
 
 // LSTM layer l of a clip range: input projection GEMM on `st`, recurrence on `rec_st`
 // (bf16 mode: gx bf16, W_hh resident on the CU).
@@ -828,7 +882,7 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
       ga.c_s0 = r.s0();
       ga.c_tn = (int)L4;
     }
-    HIPCHK(gemm<T>(ga, st, !bf));
+    HIPCHK(hgemm<T>(h, ga, st, !bf));
   }
   if (!recurrence) return VAP_OK;
   if (rec_st != st) {  // fork: the recurrence waits for the projection (ONE event from the pool)
@@ -841,6 +895,9 @@ int lstm_layer(vap_handle* h, const Plan& p, unsigned char* ws, int l, Range r, 
     if constexpr (bf) {
       if (int rc = launch_rec(h, (const bf16*)GX, r.s0(), S, (int)L4, l, (bf16*)(Hb[l & 1] + 4 * D), p.sh, rec_st, nullptr,
                               xg0))
+        return rc;
+    } else if (h->fp32_split && h->fp32_quad) {
+      if (int rc = launch_rec_f32(h, (const float*)GX, S, (int)L4, l, (float*)(Hb[l & 1] + 4 * D), p.sh, rec_st, xg0))
         return rc;
     } else
       HIPCHK(launch_lstm<T>((const float*)GX, S, (int)L4, h->W<T>("whh" + s), Hb[l & 1] + 4 * D, p.sh, rec_st));
@@ -860,7 +917,7 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
   if (h->dims.mono) {  // VapGPTMono: logits = vap_head(x) (vap/model.py:384-385); no combinator / VAD head
     Timed tm(h, VAP_K_HEADS, st);
     HIPCHK(launch_layernorm<T>(X, (int64_t)S * T_, nullptr, nullptr, 0.f, nullptr, RAW, st));  // fp32 -> storage
-    HIPCHK(gemm<T>(gargs(RAW, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, S,
+    HIPCHK(hgemm<T>(h, gargs(RAW, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, S,
                          logits + (int64_t)r.c0 * T_ * 256, 256, (int64_t)T_ * 256), st, true));
     return VAP_OK;
   }
@@ -888,7 +945,7 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
     ga.act = 2;
     ga.gamma = h->P("ar.combinator.ln.weight");
     ga.beta = h->P("ar.combinator.ln.bias");
-    HIPCHK(gemm<T>(ga, st, true));
+    HIPCHK(hgemm<T>(h, ga, st, true));
     // second half + the first's fp32 rows, stored straight in the storage type (the vap_head GEMM's
     // operand; a separate fp32 -> bf16 pass over HC cost 16 us per bench step)
     GemmArgs gb = ga;
@@ -898,8 +955,8 @@ int heads(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* logit
     gb.ld_add = D;
     gb.add_seq_stride = t1;
     gb.C = HCT;
-    HIPCHK(gemm<T>(gb, st, false));
-    HIPCHK(gemm<T>(gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
+    HIPCHK(hgemm<T>(h, gb, st, false));
+    HIPCHK(hgemm<T>(h, gargs(HCT, D, t1, h->W<T>("head"), D, 256, h->P("vap_head.bias"), T_, r.nc,
                          logits + r.c0 * (int64_t)T_ * 256, 256, (int64_t)T_ * 256), st, true));
     HIPCHK(launch_vad_head(X, r.nc, T_, h->P("va_classifier.weight"), h->P("va_classifier.bias"),
                            vadl + r.c0 * (int64_t)T_ * 2, st));
@@ -924,7 +981,7 @@ int back_end(vap_handle* h, const Plan& p, unsigned char* ws, Range r, float* lo
     ga.act = 2;
     ga.gamma = h->P("encoder.downsample.2.ln.weight");
     ga.beta = h->P("encoder.downsample.2.ln.bias");
-    HIPCHK(gemm<T>(ga, st, true));
+    HIPCHK(hgemm<T>(h, ga, st, true));
   }
   if (enc_out) {  // EncoderCPC output, (x1, x2) = channel 0 / 1 -> enc_out [2][B][T][256] ([B][T][256] mono)
     const int64_t B = p.B;
@@ -1090,6 +1147,39 @@ int launch_rec(vap_handle* h, const bf16* GX, int seq0, int S, int L4, int layer
   h->xtag += (unsigned)span;
   HIPCHK(launch_lstm_pair(GX, seq0, S, L4, h->W<bf16>("whh_pair" + s), out, out_stride, st, sy,
                           (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0, h->lstm_xplain));
+  return VAP_OK;
+}
+
+// The fp32 recurrence of S sequences on the quad-split kernel (gate rows GX [S][L4][1024] fp32, h rows to
+// out).  Shares the handle's exchange buffer and tag counter with the bf16 pair kernel (a handle runs one
+// precision); xg0 offsets the launch's slots (launches that may run concurrently use disjoint slots).
+int launch_rec_f32(vap_handle* h, const float* GX, int S, int L4, int layer, float* out, int64_t out_stride,
+                   hipStream_t st, int xg0) {
+  const std::string s = "_l" + std::to_string(layer);
+  const size_t slot = lstm_quad_xbuf_bytes(16);
+  const size_t need = (size_t)xg0 * slot + lstm_quad_xbuf_bytes(S);
+  if (need > h->xbuf_bytes) {  // grow (rare): no launch may still use the old buffer
+    HIPCHK(hipDeviceSynchronize());
+    if (h->xbuf) HIPCHK(hipFree(h->xbuf));
+    h->xbuf = nullptr;
+    h->xbuf_bytes = 0;
+    const size_t bytes = std::max(need, (size_t)8 * slot);
+    HIPCHK(hipMalloc(&h->xbuf, bytes));
+    HIPCHK(hipMemset(h->xbuf, 0, bytes));  // tags are >= 1: zero never matches
+    HIPCHK(hipDeviceSynchronize());
+    h->xbuf_bytes = bytes;
+  }
+  const uint64_t span = (uint64_t)L4 + 1;
+  if ((uint64_t)h->xtag + span + 1 > 0xFFFFFFFFull) {  // tag space exhausted: restart at 1
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemset(h->xbuf, 0, h->xbuf_bytes));
+    HIPCHK(hipDeviceSynchronize());
+    h->xtag = 0;
+  }
+  const unsigned tag0 = h->xtag + 1;
+  h->xtag += (unsigned)span;
+  HIPCHK(launch_lstm_quad(GX, S, L4, h->W<bf16>("whhq" + s), out, out_stride, st,
+                          (unsigned char*)h->xbuf + (size_t)xg0 * slot, tag0, h->err_dev));
   return VAP_OK;
 }
 
@@ -1312,7 +1402,7 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       ga.act = 2;
       ga.gamma = h->P("encoder.downsample.2.ln.weight");
       ga.beta = h->P("encoder.downsample.2.ln.bias");
-      HIPCHK(gemm<T>(ga, bs, true));
+      HIPCHK(hgemm<T>(h, ga, bs, true));
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
     const bool hchunk = h->heads_chunked && h->dims.cross_layers > 0;
@@ -1425,7 +1515,7 @@ int conv_rows(vap_handle* h, const Plan& p, const float* wav, int64_t N, unsigne
     ga.c_pair = 1;  // the pair-recurrence layout, ring slots slot .. slot + n - 1
     ga.c_t0 = (int)slot;
     ga.c_tn = (int)L[4];
-    HIPCHK(gemm<T>(ga, st, false));
+    HIPCHK(hgemm<T>(h, ga, st, false));
     r += n;
   }
   return VAP_OK;
@@ -1897,6 +1987,8 @@ int vap_create(const vap_dims* dims, vap_handle** out) {
   if (const char* e = getenv("VAP_BLOCK_FUSE")) h->block_fuse = atoi(e) != 0;
   if (const char* e = getenv("VAP_BE_SPLIT")) h->be_split = atoi(e);
   if (const char* e = getenv("VAP_LSTM_XPLAIN")) h->lstm_xplain = atoi(e);
+  if (const char* e = getenv("VAP_FP32_EXACT")) h->fp32_split = atoi(e) == 0;
+  if (const char* e = getenv("VAP_FP32_QUAD")) h->fp32_quad = atoi(e) != 0;
   if (const char* e = getenv("VAP_BE_FRAC")) {  // the caller stream's share of two back-end groups, in (0, 1)
     const double f = atof(e);
     if (!(f > 0.0 && f < 1.0)) {
@@ -1973,6 +2065,8 @@ int vap_finalize(vap_handle* h, void* stream) {
   for (auto& kv : h->fpacked) (void)hipFree(kv.second);
   h->packed.clear();
   h->fpacked.clear();
+  h->packed_numel.clear();
+  h->split_of.clear();
   const int rc = h->dims.precision == VAP_PRECISION_BF16 ? pack_all<bf16>(h, (hipStream_t)stream)
                                                           : pack_all<float>(h, (hipStream_t)stream);
   if (rc) return rc;

@@ -27,10 +27,15 @@ struct GemmArgs {
   // small_tiles = 1: the 128-row register-staged kernel even for bf16 (more workgroups for short launches;
   // chosen by the caller per call site, never by M, so outputs stay batch-invariant)
   int small_tiles = 0;
+  // split = 1 (fp32 operands, TOut float): W is the split weight [2][N][K] bf16 (hi, then lo; launch_split_bf16)
+  // and the product runs as three bf16 MFMAs per tile-step (k_gemm.hip gemm3_kernel), K % 64 == 0
+  int split = 0;
 };
 
 template <typename T, typename TOut>
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
+// fp32 [n] -> bf16 [2][n]: hi = bf16(x), lo = bf16(x - hi) (the split operands of gemm3_kernel)
+hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, hipStream_t st);
 
 // bf16 CPC conv2..4 (k4 s2 p1, 256 -> 256) + bias + ChannelNorm + ReLU (k_conv234.hip).  `in` points at
 // the buffer row 2*a of the first output row a of the range (one zero pad row in front of each
@@ -142,6 +147,14 @@ hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16*
                             int xplain = 0);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
+// fp32 parity mode: W_hh split over a QUAD of workgroups (k_lstm.hip lstm_quad_kernel), split-bf16 products:
+// gx fp32 [S][Tn][1024] (biases included), whh_quad from launch_pack_whh_quad ([4][4][64][64][8] bf16), h rows
+// fp32 to out (row t of sequence s at out + s*out_seq_stride + t*256); xbuf: lstm_quad_xbuf_bytes(S), zeroed
+// once; xtag >= 1: this launch's tags are xtag .. xtag + Tn - 1 (above every earlier launch's on the same slots)
+hipError_t launch_lstm_quad(const float* gx, int S, int Tn, const bf16* whh_quad, float* out, int64_t out_seq_stride,
+                            hipStream_t st, void* xbuf, unsigned xtag, unsigned* err);
+hipError_t launch_pack_whh_quad(const float* whh, bf16* packed, hipStream_t st);
+size_t lstm_quad_xbuf_bytes(int S);
 // The bf16 LSTM gate buffer in the pair-recurrence layout (k_lstm.hip lstm_pair_kernel): for each group of
 // 16 sequences, ring slot and 16-unit block ub = 8p + w (half p of the pair, wave w), one 2 KiB block of
 // 2 halves x 64 lanes x 16 bytes, lane = 16 lg + s % 16 holding units 16ub + 4lg .. +3 of sequence s:
@@ -178,6 +191,7 @@ struct AttnArgs {
   float scale;
   int q0 = 0;                             // queries [q0, T) against keys [0, T) (time-chunked back end;
                                           // bf16 attn3 only); Q / O still point at row 0
+  int split = 0;                          // fp32: products on split-bf16 operands (k_attn.hip attn_split_kernel)
 };
 template <typename T>
 hipError_t launch_attention(const AttnArgs& a, hipStream_t st);

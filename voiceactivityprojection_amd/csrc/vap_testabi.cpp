@@ -59,6 +59,17 @@ int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, cons
   hipStream_t st = (hipStream_t)stream;
   if (precision == VAP_PRECISION_BF16)
     return rc_of(out_f32 ? launch_gemm<bf16, float>(g, st) : launch_gemm<bf16, bf16>(g, st));
+  if (precision == 2) {  // fp32 operands through the split-bf16 kernel (the parity mode's GEMMs): W split here
+    void* ws = nullptr;
+    if (hipMalloc(&ws, (size_t)N * K * 2 * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
+    hipError_t e = launch_split_bf16((const float*)W, (bf16*)ws, (int64_t)N * K, st);
+    g.W = ws;
+    g.split = 1;
+    if (e == hipSuccess) e = launch_gemm<float, float>(g, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(ws);
+    return rc_of(e);
+  }
   return rc_of(launch_gemm<float, float>(g, st));
 }
 
@@ -90,6 +101,7 @@ int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq
                        int64_t k_seq, const void* V, int64_t v_ld, int64_t v_seq, void* O, int64_t o_ld,
                        int64_t o_seq, const float* slopes, int S, int T, int H, int kv_swap, float scale, void* stream) {
   AttnArgs a{Q, q_ld, q_seq, K, k_ld, k_seq, V, v_ld, v_seq, O, o_ld, o_seq, slopes, S, T, H, kv_swap, scale};
+  a.split = precision == 2;  // fp32 operands on split-bf16 products (the parity mode's kernel)
   hipStream_t st = (hipStream_t)stream;
   return rc_of(precision == VAP_PRECISION_BF16 ? launch_attention<bf16>(a, st) : launch_attention<float>(a, st));
 }
@@ -138,6 +150,24 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
     if (gp) (void)hipFree(gp);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(gs);
+    (void)hipFree(xb);
+    return rc_of(e);
+  }
+  if (precision == VAP_PRECISION_FP32 && variant == 4) {  // the quad split on split-bf16 operands (lstm_quad_kernel)
+    void* xb = nullptr;
+    const size_t xbytes = lstm_quad_xbuf_bytes(S);
+    if (hipMalloc(&xb, xbytes) != hipSuccess) return VAP_ERR_HIP;
+    void* wq = nullptr;
+    if (hipMalloc(&wq, (size_t)2 * 1024 * 256 * sizeof(bf16)) != hipSuccess) {
+      (void)hipFree(xb);
+      return VAP_ERR_HIP;
+    }
+    hipError_t e = hipMemsetAsync(xb, 0, xbytes, st);
+    if (e == hipSuccess) e = launch_pack_whh_quad(whh, (bf16*)wq, st);
+    if (e == hipSuccess)
+      e = launch_lstm_quad((const float*)gx, S, T, (const bf16*)wq, (float*)out, (int64_t)T * 256, st, xb, 1, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(wq);
     (void)hipFree(xb);
     return rc_of(e);
   }
