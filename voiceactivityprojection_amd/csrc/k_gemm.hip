@@ -24,9 +24,7 @@
 // (x - hi - lo ~ 2^-17 |x|), and each product as hi_a hi_w + hi_a lo_w + lo_a hi_w (the lo lo term is
 // ~2^-18 of it), three v_mfma_f32_16x16x32_bf16 with fp32 accumulation: 3 x 16 cycles per 16x16x32
 // tile-step instead of 8 x 32 for v_mfma_f32_16x16x4_f32 (5.3x the matrix rate).  W arrives pre-split
-// ([2][N][K] bf16, launch_split_bf16); A is split once per workgroup while it is staged to LDS.
-// BK = 64: A hi / lo 2 x 16 KiB + W hi / lo 2 x 32 KiB = 96 KiB, one LDS buffer (the next stage is
-// prefetched into registers during the MFMAs of this one).
+// (launch_split_bf16); A is split once per workgroup while it is staged to LDS.
 #include <cstdlib>
 
 #include "vap_common.h"
@@ -244,70 +242,61 @@ __global__ __launch_bounds__(512) void gemm_kernel(GemmArgs g) {
 
 
 // fp32 A x split W on the bf16 matrix cores (see the header): C = epi(A . W^T) at ~fp32 accuracy.
-// Staging per 64-k stage: thread t loads 4 A chunks (4 floats: row id >> 4, k 4 (id & 15)) and 4 + 4
-// W chunks (8 bf16 of the hi / lo images: row id >> 3, k 8 (id & 7)); A is split while it is stored.
-constexpr int G3_AIMG = BM * ROWB, G3_WIMG = BN * ROWB;                      // 16 KiB, 32 KiB
-constexpr int G3_LDS = 2 * G3_AIMG + 2 * G3_WIMG;                            // 96 KiB
+// Stage = 32 k.  Every staged row is 128 B = [hi of the 32 k | lo of the 32 k] (chunks 0-3 hi, 4-7 lo),
+// swizzled as the bf16 kernel's rows (chunk ^= (row>>1)&7): a wave's hi and lo fragment reads are
+// exactly that kernel's two sub-steps, conflict-free.  A stage is 48 KiB (A 16 + W 32), double-buffered
+// as in gemm_kernel (one barrier per stage; the next stage is loaded into registers during the MFMAs).
+// W arrives pre-split in the same row format ([N][K/32][64] bf16, launch_split_bf16 with K); thread t
+// stages 2 A chunks (4 floats: row id >> 3, k 4 (id & 7), split into 8-B hi / lo halves) and 4 W chunks.
 __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[G3_LDS];
-  unsigned char* Ahi = smem;
-  unsigned char* Alo = smem + G3_AIMG;
-  unsigned char* Whi = smem + 2 * G3_AIMG;
-  unsigned char* Wlo = Whi + G3_WIMG;
-
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int M = g.M_per_seq * g.n_seq;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const float* __restrict__ A = (const float*)g.A;
-  const bf16* __restrict__ Wh = (const bf16*)g.W;
-  const bf16* __restrict__ Wl = Wh + (int64_t)g.N * g.K;
+  const bf16* __restrict__ W = (const bf16*)g.W;
 
-  const float* aptr[4];
-  bool aval[4];
+  const float* aptr[2];
+  bool aval[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int id = tid + i * 512, row = id >> 4, c = id & 15;
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + i * 512, row = id >> 3, c = id & 7;
     const int m = m0 + row;
     aval[i] = m < M;
     const int mm = aval[i] ? m : 0;
     const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
     aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * 4;
   }
-  int64_t woff[4];
+  const bf16* bptr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int id = tid + i * 512, row = id >> 3, c = id & 7;
-    woff[i] = (int64_t)(n0 + row) * g.K + c * 8;
+    bptr[i] = W + (int64_t)(n0 + row) * (2 * g.K) + c * 8;
   }
-  chunk16 ra[4], rh[4], rl[4];
-  auto gload = [&](int k0) {
+  chunk16 ra[2], rb[4];
+  auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + k0) : chunk16{0, 0, 0, 0};
+    for (int i = 0; i < 2; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + kt * 32) : chunk16{0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rh[i] = *(const chunk16*)(Wh + woff[i] + k0);
-      rl[i] = *(const chunk16*)(Wl + woff[i] + k0);
-    }
+    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + kt * 64);
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + i * 512, row = id >> 4, c = id & 15;  // floats 4c .. 4c+3 = bf16 bytes 8c .. 8c+7
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + i * 512, row = id >> 3, c = id & 7;  // floats 4c .. 4c+3 -> bf16 bytes 8c .. 8c+7 of a half
       const f32x4 v = __builtin_bit_cast(f32x4, ra[i]);
       const bf16x4 hi = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       const bf16x4 lo = {(bf16)(v[0] - (float)hi[0]), (bf16)(v[1] - (float)hi[1]), (bf16)(v[2] - (float)hi[2]),
                          (bf16)(v[3] - (float)hi[3])};
-      const int off = row * ROWB + swz(row, c >> 1) * 16 + (c & 1) * 8;
-      *(bf16x4*)(Ahi + off) = hi;
-      *(bf16x4*)(Alo + off) = lo;
+      *(bf16x4*)(base + row * ROWB + swz(row, c >> 1) * 16 + (c & 1) * 8) = hi;
+      *(bf16x4*)(base + row * ROWB + swz(row, 4 + (c >> 1)) * 16 + (c & 1) * 8) = lo;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int id = tid + i * 512, row = id >> 3, c = id & 7;
-      const int off = row * ROWB + swz(row, c) * 16;
-      *(chunk16*)(Whi + off) = rh[i];
-      *(chunk16*)(Wlo + off) = rl[i];
+      *(chunk16*)(base + BM * ROWB + row * ROWB + swz(row, c) * 16) = rb[i];
     }
   };
 
@@ -317,55 +306,54 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = g.K / 64;
+  const int nk = g.K / 32;
   gload(0);
-  lstore();
+  lstore(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * 64);
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const unsigned char* abase = smem + cur * BUF;
+    const unsigned char* bbase = abase + BM * ROWB;
+    chunk16 ah[4], al[4], bh[4], bl[4];
+    const int c = lane >> 4;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      chunk16 ah[4], al[4], bh[4], bl[4];
-      const int c = sub * 4 + (lane >> 4);
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + (lane & 15);
+      ah[i] = *(const chunk16*)(abase + row * ROWB + swz(row, c) * 16);
+      al[i] = *(const chunk16*)(abase + row * ROWB + swz(row, 4 + c) * 16);
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + (lane & 15);
-        const int off = row * ROWB + swz(row, c) * 16;
-        ah[i] = *(const chunk16*)(Ahi + off);
-        al[i] = *(const chunk16*)(Alo + off);
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn * 64 + j * 16 + (lane & 15);
+      bh[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, c) * 16);
+      bl[j] = *(const chunk16*)(bbase + row * ROWB + swz(row, 4 + c) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + (lane & 15);
-        const int off = row * ROWB + swz(row, c) * 16;
-        bh[j] = *(const chunk16*)(Whi + off);
-        bl[j] = *(const chunk16*)(Wlo + off);
+        acc[i][j] = mfma_chunk<bf16>(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16>(al[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16>(ah[i], bh[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[i][j] = mfma_chunk<bf16>(ah[i], bl[j], acc[i][j]);
-          acc[i][j] = mfma_chunk<bf16>(al[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma_chunk<bf16>(ah[i], bh[j], acc[i][j]);
-        }
-    }
-    __syncthreads();  // every wave is done reading this stage
-    if (kt + 1 < nk) {
-      lstore();
-      __syncthreads();
-    }
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
   }
   gemm_epilogue<float>(g, acc, smem, m0, n0, wm, wn, lane, M);
 }
 
-// fp32 [n] -> bf16 hi [0, n) and lo [n, 2n): x = hi + lo + O(2^-17 |x|)
-__global__ void split_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out, int64_t n) {
+// fp32 W [N][K] -> the split row format of gemm3_kernel: out[n][kb][0..31] = hi, [32..63] = lo of
+// W[n][32kb .. 32kb + 31] (hi = bf16(x), lo = bf16(x - hi): x = hi + lo + O(2^-17 |x|))
+__global__ void split_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out, int64_t n, int K) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float x = in[i];
     const bf16 hi = (bf16)x;
-    out[i] = hi;
-    out[n + i] = (bf16)(x - (float)hi);
+    const int64_t row = i / K;
+    const int k = (int)(i - row * K);
+    bf16* o = out + row * 2 * K + (k >> 5) * 64 + (k & 31);
+    o[0] = hi;
+    o[32] = (bf16)(x - (float)hi);
   }
 }
 
@@ -386,8 +374,8 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   }
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   if constexpr (sizeof(T) == 4 && sizeof(TOut) == 4) {
-    if (g.split) {  // fp32 operands through the split-bf16 kernel (W: [2][N][K] bf16 from launch_split_bf16)
-      if (g.K % 64 != 0) return hipErrorInvalidValue;
+    if (g.split) {  // fp32 operands through the split-bf16 kernel (W: launch_split_bf16's row format)
+      if (g.K % 32 != 0) return hipErrorInvalidValue;
       hipLaunchKernelGGL(gemm3_kernel, grid, dim3(512), 0, st, g);
       return hipGetLastError();
     }
@@ -396,9 +384,9 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, hipStream_t st) {
-  if (n <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(split_bf16_kernel, dim3(256), dim3(256), 0, st, in, out, n);
+hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, int K, hipStream_t st) {
+  if (n <= 0 || K <= 0 || K % 32 || n % K) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(256), dim3(256), 0, st, in, out, n, K);
   return hipGetLastError();
 }
 

@@ -853,8 +853,10 @@ VAP_DEV void quad_steps(const float* __restrict__ gxs, int Tn, int S, const chun
           xv[p][1] = xload(xr, xoff((Q + 1 + p) & 3, par, 1));
         }
         const int uq = 64 * ((Q + 1 + p) & 3) + 16 * w + 4 * (lane >> 4);  // the partner lane's units
-        hput(uq, __builtin_bit_cast(float, xv[p][0][0]), __builtin_bit_cast(float, xv[p][0][2]),
-             __builtin_bit_cast(float, xv[p][1][0]), __builtin_bit_cast(float, xv[p][1][2]));
+        // (bit-cast whole vectors: hipcc lowers __builtin_bit_cast(float, v[i]) of an ext_vector element to
+        // element 0 whatever i is, vap_common.h)
+        const f32x4 v0 = __builtin_bit_cast(f32x4, xv[p][0]), v1 = __builtin_bit_cast(f32x4, xv[p][1]);
+        hput(uq, v0[0], v0[2], v1[0], v1[2]);
       }
     }
     // (barriers as asm with a memory clobber: the s_barrier builtin does not order the LDS reads after it)

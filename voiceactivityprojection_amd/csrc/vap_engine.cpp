@@ -106,7 +106,7 @@ struct vap_handle {
   // fp32 parity mode: GEMMs on split-bf16 operands (k_gemm.hip gemm3_kernel; VAP_FP32_EXACT=1: the exact
   // fp32-MFMA kernels); fp32 packed weight -> its split copy [2][N][K] bf16
   bool fp32_split = true;
-  bool fp32_quad = false;  // VAP_FP32_QUAD=1: the recurrence on the quad-split kernel (k_lstm.hip lstm_quad_kernel)
+  bool fp32_quad = true;  // VAP_FP32_QUAD=0: the recurrence on lstm_kernel<float> instead of the quad split
   std::map<const void*, const void*> split_of;
   std::map<std::string, int64_t> packed_numel;
   unsigned epoch = 0;
@@ -600,10 +600,13 @@ int pack_all(vap_handle* h, hipStream_t st) {
     for (auto& kv : h->packed_numel)
       if (kv.first.rfind("whh", 0) != 0) todo.push_back(kv);
     for (auto& kv : todo) {
+      const std::string& n = kv.first;  // the GEMM's K (the weight's row length) by weight
+      const int K = n.rfind("conv", 0) == 0 ? kws[n[4] - '0'] * D : n == "down" ? 5 * D
+                    : (n.size() > 3 && n.compare(n.size() - 3, 3, ".w2") == 0) ? 3 * D : D;
       void* sp = nullptr;
       if (hipMalloc(&sp, kv.second * 2 * sizeof(bf16)) != hipSuccess) return fail(VAP_ERR_HIP, "hipMalloc split weight");
       h->packed[kv.first + "@s"] = sp;
-      HIPCHK(launch_split_bf16((const float*)h->packed.at(kv.first), (bf16*)sp, kv.second, st));
+      HIPCHK(launch_split_bf16((const float*)h->packed.at(kv.first), (bf16*)sp, kv.second, K, st));
       h->split_of[h->packed.at(kv.first)] = sp;
     }
   }

@@ -27,15 +27,16 @@ struct GemmArgs {
   // small_tiles = 1: the 128-row register-staged kernel even for bf16 (more workgroups for short launches;
   // chosen by the caller per call site, never by M, so outputs stay batch-invariant)
   int small_tiles = 0;
-  // split = 1 (fp32 operands, TOut float): W is the split weight [2][N][K] bf16 (hi, then lo; launch_split_bf16)
-  // and the product runs as three bf16 MFMAs per tile-step (k_gemm.hip gemm3_kernel), K % 64 == 0
+  // split = 1 (fp32 operands, TOut float): W is the split weight [N][K/32][64] bf16 (launch_split_bf16) and the
+  // product runs as three bf16 MFMAs per tile-step (k_gemm.hip gemm3_kernel), K % 32 == 0
   int split = 0;
 };
 
 template <typename T, typename TOut>
 hipError_t launch_gemm(const GemmArgs& g, hipStream_t st);
-// fp32 [n] -> bf16 [2][n]: hi = bf16(x), lo = bf16(x - hi) (the split operands of gemm3_kernel)
-hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, hipStream_t st);
+// fp32 W [n / K][K] -> bf16 [n / K][K / 32][64]: per 32-k block hi = bf16(x) then lo = bf16(x - hi) (the split
+// weight rows of gemm3_kernel)
+hipError_t launch_split_bf16(const float* in, bf16* out, int64_t n, int K, hipStream_t st);
 
 // bf16 CPC conv2..4 (k4 s2 p1, 256 -> 256) + bias + ChannelNorm + ReLU (k_conv234.hip).  `in` points at
 // the buffer row 2*a of the first output row a of the range (one zero pad row in front of each

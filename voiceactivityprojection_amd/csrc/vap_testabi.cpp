@@ -62,7 +62,7 @@ int vap_test_gemm(int precision, const void* A, int64_t lda, int64_t a_seq, cons
   if (precision == 2) {  // fp32 operands through the split-bf16 kernel (the parity mode's GEMMs): W split here
     void* ws = nullptr;
     if (hipMalloc(&ws, (size_t)N * K * 2 * sizeof(bf16)) != hipSuccess) return VAP_ERR_HIP;
-    hipError_t e = launch_split_bf16((const float*)W, (bf16*)ws, (int64_t)N * K, st);
+    hipError_t e = launch_split_bf16((const float*)W, (bf16*)ws, (int64_t)N * K, K, st);
     g.W = ws;
     g.split = 1;
     if (e == hipSuccess) e = launch_gemm<float, float>(g, st);
