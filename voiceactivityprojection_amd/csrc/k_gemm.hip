@@ -26,6 +26,7 @@
 // tile-step instead of 8 x 32 for v_mfma_f32_16x16x4_f32 (5.3x the matrix rate).  W arrives pre-split
 // (launch_split_bf16); A is split once per workgroup while it is staged to LDS.
 #include <cstdlib>
+#include <type_traits>
 
 #include "vap_common.h"
 #include "vap_kernels.h"
@@ -254,34 +255,41 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
   const int wm = wave & 1, wn = wave >> 1;
   const int M = g.M_per_seq * g.n_seq;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const float* __restrict__ A = (const float*)g.A;
-  const bf16* __restrict__ W = (const bf16*)g.W;
+  const float* A = (const float*)g.A;
+  const bf16* W = (const bf16*)g.W;
 
-  const float* aptr[2];
-  bool aval[2];
+  // loads through buffer resources: one 32-bit lane offset per chunk, the stage as a scalar offset; A rows
+  // past M read as zero (offset outside the resource), no branches (a conditional load made the compiler
+  // drain every load in flight); A's resource starts at the tile's first sequence (the host checks that
+  // the tile's rows lie within the 2 GiB a buffer offset reaches)
+  const int sq0 = m0 / g.M_per_seq;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(A + (int64_t)sq0 * g.a_seq_stride, 0x7FFFFFF0u);
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, 0x7FFFFFF0u);
+  uint32_t aoff[2], woff[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int id = tid + i * 512, row = id >> 3, c = id & 7;
     const int m = m0 + row;
-    aval[i] = m < M;
-    const int mm = aval[i] ? m : 0;
-    const int s = mm / g.M_per_seq, t = mm - s * g.M_per_seq;
-    aptr[i] = A + (int64_t)s * g.a_seq_stride + (int64_t)t * g.lda + c * 4;
+    const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+    aoff[i] = m < M ? (uint32_t)((((int64_t)(s - sq0) * g.a_seq_stride + (int64_t)t * g.lda) + c * 4) * 4) : 0x80000000u;
   }
-  const bf16* bptr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int id = tid + i * 512, row = id >> 3, c = id & 7;
-    bptr[i] = W + (int64_t)(n0 + row) * (2 * g.K) + c * 8;
+    woff[i] = (uint32_t)(((int64_t)(n0 + row) * (2 * g.K) + c * 8) * 2);
   }
-  chunk16 ra[2], rb[4];
-  auto gload = [&](int kt) {
+  // A (streamed from HBM) is prefetched three stages ahead through a ring of register sets, W (L2-resident,
+  // small) one stage ahead: issued W(k+1) first, then A(k+3), so the wait for W(k+1) leaves A(k+3) in flight
+  chunk16 ra[3][2], rb[4];
+  auto gloadA = [&](int kt, chunk16 (&r)[2]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ra[i] = aval[i] ? *(const chunk16*)(aptr[i] + kt * 32) : chunk16{0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rb[i] = *(const chunk16*)(bptr[i] + kt * 64);
+    for (int i = 0; i < 2; ++i) r[i] = buf_load16(rA, aoff[i], (uint32_t)kt * 128u);
   };
-  auto lstore = [&](int buf) {
+  auto gloadW = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb[i] = buf_load16(rW, woff[i], (uint32_t)kt * 128u);
+  };
+  auto lstore = [&](int buf, const chunk16 (&ra)[2]) {
     unsigned char* base = smem + buf * BUF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -307,12 +315,17 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / 32;
-  gload(0);
-  lstore(0);
+  gloadW(0);
+  gloadA(0, ra[0]);
+  if (nk > 1) gloadA(1, ra[1]);
+  if (nk > 2) gloadA(2, ra[2]);
+  lstore(0, ra[0]);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
+  auto stage = [&](int kt, auto slot) {
+    constexpr int S0 = decltype(slot)::value, S1 = (S0 + 1) % 3;  // ring slots of stages kt (and kt+3), kt+1
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) gloadW(kt + 1);
+    if (kt + 3 < nk) gloadA(kt + 3, ra[S0]);
     const unsigned char* abase = smem + cur * BUF;
     const unsigned char* bbase = abase + BM * ROWB;
     chunk16 ah[4], al[4], bh[4], bl[4];
@@ -337,8 +350,13 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemmArgs g) {
         acc[i][j] = mfma_chunk<bf16>(al[i], bh[j], acc[i][j]);
         acc[i][j] = mfma_chunk<bf16>(ah[i], bh[j], acc[i][j]);
       }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    if (kt + 1 < nk) lstore(cur ^ 1, ra[S1]);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 3) {
+    stage(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nk) stage(kt + 1, std::integral_constant<int, 1>{});
+    if (kt + 2 < nk) stage(kt + 2, std::integral_constant<int, 2>{});
   }
   gemm_epilogue<float>(g, acc, smem, m0, n0, wm, wn, lane, M);
 }
@@ -376,6 +394,10 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
   if constexpr (sizeof(T) == 4 && sizeof(TOut) == 4) {
     if (g.split) {  // fp32 operands through the split-bf16 kernel (W: launch_split_bf16's row format)
       if (g.K % 32 != 0) return hipErrorInvalidValue;
+      // a tile's A rows (at most BM / M_per_seq + 2 sequences) and the split W lie within a buffer offset's 2 GiB
+      if ((((int64_t)BM / g.M_per_seq + 2) * g.a_seq_stride + (int64_t)BM * g.lda + g.K) * 4 >= 0x7FFFFFF0LL ||
+          (int64_t)g.N * g.K * 4 >= 0x7FFFFFF0LL)
+        return hipErrorInvalidValue;
       hipLaunchKernelGGL(gemm3_kernel, grid, dim3(512), 0, st, g);
       return hipGetLastError();
     }
