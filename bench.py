@@ -466,7 +466,7 @@ def _leg(model, wav, steps: int, warmup: int, keys=None):
     return (time.perf_counter() - t0) / steps * 1e3, out
 
 
-def extras(args, model, dev, sd_np, steps: int = 3, warmup: int = 2):
+def extras(args, model, dev, sd_np, steps: int = 5, warmup: int = 3):
     """Secondary BASELINE configurations measured in the same run after the headline (N = 1, untimed by
     the headline): C4 (32 x 60 s, T = 3000, the headline's precision) and the fp32 parity mode on the
     headline workload (64 x 20 s) with its errors against the reference fixture."""

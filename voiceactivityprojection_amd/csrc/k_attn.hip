@@ -453,31 +453,52 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // K / V of the next key block are loaded into registers while this one computes (buffer loads: keys
+  // >= T read as zero); thread item it = tid + 256 i covers keys 2 (it >> 4) and +1, floats 4 (it & 15) .. +3,
+  // so V^T takes one 4-byte write per (d, key pair) and K one 8-byte write per row and half
+  const __amdgpu_buffer_rsrc_t rK = make_rsrc(Ks, (uint32_t)((int64_t)a.T * a.k_ld * 4));
+  const __amdgpu_buffer_rsrc_t rV = make_rsrc(Vs, (uint32_t)((int64_t)a.T * a.v_ld * 4));
+  f32x4 kr[2][2], vr[2][2];
+  auto kvload = [&](int key0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int it = tid + 256 * i, key = key0 + 2 * (it >> 4), c = it & 15;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        kr[i][e] = __builtin_bit_cast(f32x4, buf_load16(rK, (uint32_t)(((int64_t)(key + e) * a.k_ld + c * 4) * 4), 0));
+        vr[i][e] = __builtin_bit_cast(f32x4, buf_load16(rV, (uint32_t)(((int64_t)(key + e) * a.v_ld + c * 4) * 4), 0));
+      }
+    }
+  };
+  kvload(0);
   for (int kb = 0; kb <= qb; ++kb) {
     const int key0 = kb * KB;
     // ---- stage K hi / lo [key][d] (8-B halves of swizzled 16-B chunks) and V^T hi / lo [d][key]
-    for (int i = tid; i < KB * 16; i += 256) {
-      const int row = i >> 4, c = i & 15;  // floats 4c .. 4c+3 of key row `row`
-      const int key = key0 + row;
-      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
-      if (key < a.T) {
-        kv = *(const f32x4*)(Ks + (int64_t)key * a.k_ld + c * 4);
-        vv = *(const f32x4*)(Vs + (int64_t)key * a.v_ld + c * 4);
-      }
-      const bf16x4 khi = {(bf16)kv[0], (bf16)kv[1], (bf16)kv[2], (bf16)kv[3]};
-      const bf16x4 klo = {(bf16)(kv[0] - (float)khi[0]), (bf16)(kv[1] - (float)khi[1]), (bf16)(kv[2] - (float)khi[2]),
-                          (bf16)(kv[3] - (float)khi[3])};
-      const int off = row * 128 + kswz2(row, c >> 1) * 16 + (c & 1) * 8;
-      *(bf16x4*)(skh + off) = khi;
-      *(bf16x4*)(skl + off) = klo;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16 vh = (bf16)vv[e];
-        *(bf16*)(svh + (c * 4 + e) * SVROW + row * 2) = vh;
-        *(bf16*)(svl + (c * 4 + e) * SVROW + row * 2) = (bf16)(vv[e] - (float)vh);
+    for (int i = 0; i < 2; ++i) {
+      const int it = tid + 256 * i, row = 2 * (it >> 4), c = it & 15;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x4 kv = kr[i][e];
+        const bf16x4 khi = {(bf16)kv[0], (bf16)kv[1], (bf16)kv[2], (bf16)kv[3]};
+        const bf16x4 klo = {(bf16)(kv[0] - (float)khi[0]), (bf16)(kv[1] - (float)khi[1]),
+                            (bf16)(kv[2] - (float)khi[2]), (bf16)(kv[3] - (float)khi[3])};
+        const int off = (row + e) * 128 + kswz2(row + e, c >> 1) * 16 + (c & 1) * 8;
+        *(bf16x4*)(skh + off) = khi;
+        *(bf16x4*)(skl + off) = klo;
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const float v0 = vr[i][0][d], v1 = vr[i][1][d];
+        const bf16 h0 = (bf16)v0, h1 = (bf16)v1;
+        const bf16 l0 = (bf16)(v0 - (float)h0), l1 = (bf16)(v1 - (float)h1);
+        typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        *(bf16x2*)(svh + (c * 4 + d) * SVROW + row * 2) = bf16x2{h0, h1};
+        *(bf16x2*)(svl + (c * 4 + d) * SVROW + row * 2) = bf16x2{l0, l1};
       }
     }
     __syncthreads();
+    if (kb < qb) kvload(key0 + KB);  // the next block flies while this one computes
 
     // ---- S^T tiles: st[kt][r] = score (log2 domain) of key key0 + kt*16 + (lane>>4)*4 + r, query q
     f32x4 st[4];

@@ -129,23 +129,34 @@ VAP_DEV void gemm_epilogue(const GemmArgs& g, f32x4 (&acc)[4][4], unsigned char*
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] = gelu_erf(acc[i][j][r]);
   }
+  // store: each 16-row slab of the wave's 64 x 64 block is transposed through a wave-private LDS area
+  // ([16][68] floats; rows padded so the scalar writes of two 16-lane row groups hit distinct banks), so
+  // every lane then holds 4 consecutive columns of one row: 16-B loads of the addend and 16-B stores, 256
+  // contiguous bytes per 16 lanes (the accumulator layout gave one 4-B element per lane, 64-B segments)
   TOut* __restrict__ C = (TOut*)g.C;
+  float* tp = (float*)(smem + 4096) + (wm * 4 + wn) * (16 * 68);
+  const int cl = (lane & 15) * 4;  // the lane's 4 columns of the wave's 64 after the transpose
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
-      const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
-      TOut* crow = C + (int64_t)s * g.c_seq_stride + (int64_t)t * g.ldc;
-      const float* arow = g.add ? g.add + (int64_t)s * g.add_seq_stride + (int64_t)t * g.ld_add : nullptr;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = acc[i][j][r];
-        if (arow) v += arow[colb + j * 16];
-        crow[colb + j * 16] = from_f32<TOut>(v);
+      for (int r = 0; r < 4; ++r) tp[((lane >> 4) * 4 + r) * 68 + j * 16 + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rr = p * 4 + (lane >> 4);  // row of the slab
+      f32x4 v = *(const f32x4*)(tp + rr * 68 + cl);
+      const int m = m0 + wm * 64 + i * 16 + rr;
+      if (m < M) {
+        const int s = m / g.M_per_seq, t = m - s * g.M_per_seq;
+        const int col = n0 + wn * 64 + cl;
+        if (g.add) v += *(const f32x4*)(g.add + (int64_t)s * g.add_seq_stride + (int64_t)t * g.ld_add + col);
+        store4(C + (int64_t)s * g.c_seq_stride + (int64_t)t * g.ldc + col, v[0], v[1], v[2], v[3]);
       }
     }
+    __builtin_amdgcn_wave_barrier();  // the slab is read before the next one overwrites it
+  }
 }
 
 template <typename T, typename TOut>
@@ -390,6 +401,11 @@ hipError_t launch_gemm(const GemmArgs& g, hipStream_t st) {
     // batch (or shard of a batch) it runs in -- the 128-row kernel accumulates in another order.
     if (aligned && !g.small_tiles) return launch_gemm2<TOut>(g, st);
   }
+  // the epilogue's 16-B (fp32) / 8-B (bf16) row stores and addend loads need aligned rows
+  const uintptr_t al = 4 * sizeof(TOut) - 1;
+  if (g.ldc % 4 || g.c_seq_stride % 4 || ((uintptr_t)g.C & al) ||
+      (g.add && (g.ld_add % 4 || g.add_seq_stride % 4 || ((uintptr_t)g.add & 15))))
+    return hipErrorInvalidValue;
   dim3 grid((M + BM - 1) / BM, g.N / BN);
   if constexpr (sizeof(T) == 4 && sizeof(TOut) == 4) {
     if (g.split) {  // fp32 operands through the split-bf16 kernel (W: launch_split_bf16's row format)
