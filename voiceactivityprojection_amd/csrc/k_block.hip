@@ -48,6 +48,22 @@ template <int MT> struct Blk {
 // MFMA fragment read (16 rows, lane groups of ds_read_b128) over distinct bank groups
 VAP_DEV int xswz(int row, int c) { return c ^ (row & 15); }
 
+// Row j*16 + l16 of a panel from the accumulator layout: a / b = the lane's 4 columns 32w + 4lg .. and
+// 32w + 16 + 4lg .. as packed bf16.  v_permlane16_swap trades the two 16-column blocks between lane
+// groups, so each lane holds 8 consecutive columns (32w + 16(lg & 1) + 8(lg >> 1) ..) and writes them as
+// ONE 16-B chunk: conflict-free (8-lane groups of ds_write_b128 cover 8 distinct rows' swizzled chunks),
+// where the two 8-B halves per lane put two lanes of each 16-lane group on one bank pair.
+VAP_DEV void panel_put(unsigned char* img, int row, int w, int lg, u32x2 a, u32x2 b) {
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto sw = __builtin_amdgcn_permlane16_swap(a[d], b[d], false, false);
+    a[d] = sw[0];
+    b[d] = sw[1];
+  }
+  const int c = w * 4 + (lg & 1) * 2 + (lg >> 1);
+  *(u32x4*)(img + row * ROWB + xswz(row, c) * 16) = u32x4{a[0], a[1], b[0], b[1]};
+}
+
 // GELU in sigmoid form, x * sigmoid(-x (c1 + c2 x^2) ln 2), with c1 / c2 fitted to the erf GELU
 // (max |error| 2.7e-4 over the reals, below half a bf16 ulp for |x| >= 0.14): one v_exp + one v_rcp
 // + 5 VALU.  Large negative x: exp2 -> +inf, rcp -> 0, result -0; large positive: x.
@@ -126,17 +142,19 @@ VAP_DEV void ln_panel(const f32x4 (&acc)[2][MT], float* red0, float* red1, const
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < MT; ++j) rstd[j] = rsqrtf(rowtot(red1, j) * (1.0f / D) + eps);
+    u32x2 yp[2][MT];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int n = w * 32 + i * 16 + lg * 4;
       const f32x4 ga = *(const f32x4*)(GB + n), be = *(const f32x4*)(GB + 256 + n);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        const int row = j * 16 + l16;
         const f32x4 y = (acc[i][j] - mean[j]) * rstd[j] * ga + be;
-        *(u32x2*)(P + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = pack_bf16x4(y[0], y[1], y[2], y[3]);
+        yp[i][j] = pack_bf16x4(y[0], y[1], y[2], y[3]);
       }
     }
+#pragma unroll
+    for (int j = 0; j < MT; ++j) panel_put(P, j * 16 + l16, w, lg, yp[0][j], yp[1][j]);
   }
 }
 
@@ -319,14 +337,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     __syncthreads();  // every wave is done reading H (the O panel / the previous slice)
     stamp(5 + 4 * s);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = w * 32 + i * 16 + lg * 4;
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int row = j * 16 + l16;
-        *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) = hb[i][j];
-      }
-    }
+    for (int j = 0; j < MT; ++j) panel_put(H, j * 16 + l16, w, lg, hb[0][j], hb[1][j]);
     __syncthreads();  // slice s of the hidden complete
     stamp(6 + 4 * s);
 #pragma unroll
@@ -374,15 +385,9 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     if (tidb < 128) *(f32x4*)(GB + tidb * 4) = gb2;
     if constexpr (NR2 > 0) {  // raw rows (bf16) -> H
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int n = w * 32 + i * 16 + lgb * 4;
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-          const int row = j * 16 + l16b;
-          *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
-              pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-        }
-      }
+      for (int j = 0; j < MT; ++j)
+        panel_put(H, j * 16 + l16b, w, lgb, pack_bf16x4(acc[0][j][0], acc[0][j][1], acc[0][j][2], acc[0][j][3]),
+                  pack_bf16x4(acc[1][j][0], acc[1][j][1], acc[1][j][2], acc[1][j][3]));
     }
     __builtin_amdgcn_sched_barrier(0);
     ln_panel<MT>(acc, red0, red1, GB, P, w, l16b, lgb, g.eps);
@@ -619,15 +624,9 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
   }
   if constexpr (NR > 0) {  // raw rows (bf16) -> H
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = w * 32 + i * 16 + lg * 4;
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int row = j * 16 + l16;
-        *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
-            pack_bf16x4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      }
-    }
+    for (int j = 0; j < MT; ++j)
+      panel_put(H, j * 16 + l16, w, lg, pack_bf16x4(acc[0][j][0], acc[0][j][1], acc[0][j][2], acc[0][j][3]),
+                pack_bf16x4(acc[1][j][0], acc[1][j][1], acc[1][j][2], acc[1][j][3]));
   }
   __builtin_amdgcn_sched_barrier(0);
   ln_panel<MT>(acc, red0, red1, GB, P, w, l16, lg, g.eps);
@@ -884,15 +883,9 @@ __global__ __launch_bounds__(512, 1) void heads_kernel(HeadsArgs g) {
   __builtin_amdgcn_sched_barrier(0);
   // h -> bf16 panel (H: every wave finished its x1 k-steps before the LayerNorms' barriers)
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int n = w * 32 + i * 16 + lg * 4;
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int row = j * 16 + l16;
-      *(u32x2*)(H + row * ROWB + xswz(row, n >> 3) * 16 + ((n >> 2) & 1) * 8) =
-          pack_bf16x4(h[i][j][0], h[i][j][1], h[i][j][2], h[i][j][3]);
-    }
-  }
+  for (int j = 0; j < MT; ++j)
+    panel_put(H, j * 16 + l16, w, lg, pack_bf16x4(h[0][j][0], h[0][j][1], h[0][j][2], h[0][j][3]),
+              pack_bf16x4(h[1][j][0], h[1][j][1], h[1][j][2], h[1][j][3]));
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
