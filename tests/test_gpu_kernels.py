@@ -172,13 +172,15 @@ def test_attention(prec, kv_swap):
 
 
 @pytest.mark.parametrize("prec,variant,S", [("fp32", 0, 20), ("bf16", 0, 20), ("bf16", 1, 20), ("bf16", 2, 20),
-                                            ("bf16", 3, 20), ("bf16", 3, 300), ("fp32", 4, 20), ("fp32", 4, 300)])
+                                            ("bf16", 3, 20), ("bf16", 3, 300), ("bf16", 5, 20), ("bf16", 5, 300),
+                                            ("fp32", 4, 20), ("fp32", 4, 300)])
 def test_lstm(prec, variant, S):
     """variant 0 = the resident kernel for that precision (bf16: W_hh resident in AGPR/VGPR/LDS,
     bf16 gx); variant 1 = the L2-streaming kernel in bf16 (fp32 gx); variant 2 = the resident bf16
     path with gate scales folded into W_hh and gx (the ABI scales gx), exp2-domain cell; variant 3 =
     the engine's default: W_hh split over workgroup pairs that exchange h halves every step (S = 300:
-    19 pairs, a padding pair in the last 16-block group); fp32 variant 4 = the parity mode's default: W_hh
+    19 pairs, a padding pair in the last 16-block group); variant 5 = the same operands on workgroup quads
+    (lstm_quadb_kernel, VAP_LSTM_QUAD); fp32 variant 4 = the parity mode's default: W_hh
     split over workgroup quads, split-bf16 products, fp32 gates / state / h (S = 300: 19 quads, padding
     quads in the last 32-block group)."""
     N = lib()
@@ -186,12 +188,12 @@ def test_lstm(prec, variant, S):
     g = torch.Generator().manual_seed(3)
     T = 37
     gx = torch.randn(S, T, 1024, generator=g)
-    if prec == "bf16" and variant in (0, 2, 3):
+    if prec == "bf16" and variant in (0, 2, 3, 5):
         gx = gx.to(torch.bfloat16).float()
     whh = (torch.rand(1024, 256, generator=g) * 2 - 1) / 16
     out = torch.zeros(S, T, 256, device="cuda", dtype=dt)
     packed = torch.zeros(1024 * 256, device="cuda", dtype=dt)
-    gxd = gx.cuda().to(torch.bfloat16) if (prec == "bf16" and variant in (0, 2, 3)) else gx.cuda()
+    gxd = gx.cuda().to(torch.bfloat16) if (prec == "bf16" and variant in (0, 2, 3, 5)) else gx.cuda()
     whd = whh.cuda()
     _run(N.lib().vap_test_lstm, code, _p(gxd), S, T, _p(whd), _p(packed), _p(out), variant, _st())
     wr = whh.to(dt).float()

@@ -739,6 +739,291 @@ __global__ __launch_bounds__(512, 2) void lstm_pair_kernel(const bf16* __restric
 
 
 // ------------------------------------------------------------------------------------------
+// bf16 perf mode, W_hh split over a QUAD of workgroups (VAP_LSTM_QUAD): four CUs per 16 sequences.
+//
+// The pair kernel spends ~1k cycles of MFMA and ~1k of cell update per SIMD and step (two waves per
+// SIMD in the same phase).  Here quarter q of a quad owns hidden units [64q, 64q + 64): 4 gates x 64
+// units = 256 W_hh rows = 128 KiB bf16 in registers across 4 waves (one per SIMD, 32 fragments each;
+// wave w owns units 64q + 16w .. +16, one row tile per gate), so per SIMD and step the matrix work
+// and the cell update both halve (32 MFMAs and 4 cells per lane) at the price of three exchange
+// partners instead of one.  Same operands as the pair kernel: the pair-packed W_hh (pair half p,
+// wave w' is quarter 2p + w'/4, wave w' % 4) and the pair-layout gate rows (a lane's 16-unit block
+// is 4q + w, the same records).  Exchange as lstm_pair_kernel with three partners: one 16-byte
+// {2 x bf16, tag} x 2 granule per lane and step into the quad's slot [quarter][parity][tid], polled
+// by the same lane of each partner (sc1 loads) and issued before the own-unit k-steps (2 of 8).  The
+// XCC handshake covers the whole quad (plain stores only when all four quarters share an XCD).
+// Quads are blocks (b, b+8, b+16, b+24) of each 32-block group; every spin is bounded.
+// ------------------------------------------------------------------------------------------
+constexpr int QB_NW = 4, QB_NF = 32;            // waves per workgroup, W fragments per wave
+constexpr int QB_SLOT = 4 * 2 * 256;            // 16-byte exchange slots per quad: [quarter][parity][tid]
+static_assert(QB_SLOT == P_SLOT, "the quad and pair kernels share the exchange buffer sizing");
+
+template <bool ST>
+__global__ __launch_bounds__(256, 1) void lstm_quadb_kernel(const bf16* __restrict__ gx, int seq0, int S, int Tn,
+                                                            const chunk16* __restrict__ wp, bf16* __restrict__ out,
+                                                            int64_t out_seq_stride, LstmSync sync, u32x4* xbuf) {
+  __shared__ __attribute__((aligned(16))) unsigned char hb[NS * 512];  // h_{t-1} [seq][256], chunk ^= seq
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int grp = (b >> 5) * 8 + (b & 7), q = (b >> 3) & 3;
+  if (grp * NS >= S) return;  // padding quad (all four quarters leave)
+  const int sl = lane & 15;
+  const int seq = grp * NS + sl;
+  const bool valid = seq < S;
+  const int u0 = 64 * q + 16 * w + 4 * (lane >> 4);  // this lane's 4 units
+
+  chunk16 wa[QB_NF];  // fragment f = g*8 + kk: rows g*256 + 64q + 16w + (lane&15), k = 32kk + 8(lane>>4) + e
+  const chunk16* wsrc = wp + (int64_t)(q * QB_NW + w) * QB_NF * 64 + lane;  // pair packing, (p, w') = (q/2, 4(q%2) + w)
+#pragma unroll
+  for (int f = 0; f < QB_NF; ++f) wa[f] = wsrc[f * 64];
+  for (int i = tid; i < NS * 512 / 4; i += 256) ((unsigned*)hb)[i] = 0u;  // h_{-1} = 0
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xbuf + (int64_t)grp * QB_SLOT, (uint32_t)(QB_SLOT * 16));
+  auto xoff = [&](int qq, int par) -> uint32_t { return (uint32_t)(((qq * 2 + par) * 256 + tid) * 16); };
+  const uint32_t tag_base = sync.xtag + 1u;  // tag of step t: tag_base + t; the handshake's: sync.xtag (never 0)
+
+  int ra = 0, rb = -1;
+  if (sync.ready) {
+    if (sync.time_mode) {
+      rb = 0;
+    } else {
+      const int s_first = grp * NS, s_last = min(S, s_first + NS) - 1;
+      while (sync.seq_end[ra] <= s_first) ++ra;
+      rb = ra;
+      while (sync.seq_end[rb] <= s_last) ++rb;
+    }
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (int r = ra; r <= rb; ++r)
+        while (__hip_atomic_load(sync.ready + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
+          __builtin_amdgcn_s_sleep(8);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+        }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  const int gs = seq0 + (valid ? seq : 0);
+  const bf16* gxs = gx + gx_pair_block(gs >> 4, 0, u0 >> 4, Tn) + (((u0 >> 2) & 3) * 16 + (gs & 15)) * 8;
+  const int goff = sync.gx_off;
+  auto grow = [&](int t) -> int64_t {
+    const int r = t + goff;
+    return (int64_t)(r >= Tn ? r - Tn : r) * (16 * 1024);
+  };
+  // Every vector-memory op of the step loop is inline asm in a fixed order with hand-counted waits (as
+  // lstm_pair_kernel; the compiler's own accounting falls back to vmcnt(0) at the loop's merge points,
+  // which would make the gx wait also wait for the polls just issued).  Per step t (steady state):
+  //   P  3 exchange polls (partners' h_{t-1}, t > 0) | G  gx record of step t+2 (2 loads) | R  retries
+  //   X  exchange publish (h_t)                        | O  h_t row store
+  // -> the poll wait is vmcnt(2) (G may stay in flight); gx of step t (issued in step t-2) is waited with
+  // vmcnt(9) (X O of step t-2 and P G X O of step t-1 are younger).  Retries only add younger ops.
+  auto gload = [&](u32x4 (&gv)[2], int row) {  // gates 0/1 and 2/3 of the lane's 4 units
+    const bf16* a = gxs + grow(row);
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[0]) : "v"(a) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(gv[1]) : "v"(a) : "memory");
+  };
+  auto poll = [&](u32x4& v, uint32_t off) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(xr) : "memory");
+  };
+  __syncthreads();  // hb zeroed; ready acquired
+
+  auto hfrag = [&](int kk) -> chunk16 {
+    return *(const chunk16*)(hb + sl * 512 + (((kk * 4 + (lane >> 4)) ^ sl) << 4));
+  };
+  auto hput = [&](int u, u32x2 v) { *(u32x2*)(hb + sl * 512 + (((u >> 3) ^ sl) << 4) + (u & 7) * 2) = v; };
+  const bool samp = ST && blockIdx.x < 8 && tid == 0;
+  __shared__ unsigned long long stl[ST ? 20 : 1];
+  auto stamp = [&](int t, int k) {
+    if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long v = __builtin_amdgcn_s_memtime();
+      if (samp && t >= sync.stamp_t0 && t < sync.stamp_t0 + 4) stl[(t - sync.stamp_t0) * 5 + k] = v;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const __amdgpu_buffer_rsrc_t orsc =
+      make_rsrc(out + (int64_t)grp * NS * out_seq_stride, (uint32_t)((int64_t)min(NS, S - grp * NS) * out_seq_stride * 2));
+  const uint32_t o_lane = (uint32_t)(((int64_t)sl * out_seq_stride + u0) * 2);  // missing sequences: out of range
+
+  // XCC handshake over the quad (see lstm_pair_kernel): plain exchange stores only when all four
+  // quarters run on one XCD; the parity-1 slots carry the ids under a tag no step uses.
+  bool xl2 = sync.xplain > 0;
+  if (sync.xplain == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    const uint32_t htag = tag_base - 1u;
+    buf_store16_wt(xr, xoff(q, 1), u32x4{xcc, htag, xcc, htag});
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true, same = true;
+    for (int p = 1; p < 4 && ok; ++p) {
+      while (true) {
+        const u32x4 pv = xload(xr, xoff((q + p) & 3, 1));
+        if (__all(pv[1] == htag && pv[3] == htag)) {
+          same = same && __all(pv[0] == xcc && pv[2] == xcc);
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+          if (sync.error && lane == 0) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    xl2 = ok && same;
+    if (tid == 0 && b < 64) g_lstm_xcc[b] = xcc | ((uint32_t)xl2 << 16) | (1u << 24);
+  }
+  u32x4 ga[2], gb[2];  // gx ring: ga for even steps, gb for odd
+  gload(ga, 0);
+  gload(gb, Tn > 1 ? 1 : 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the step loop's hand-counted waits start from zero
+  // settle the W fragment loads in the compiler's own bookkeeping here (an asm use makes it wait for
+  // them): left pending, it re-waits for them inside the step loop with counts that include the loop's
+  // hand-issued polls and gx loads
+#pragma unroll
+  for (int f = 0; f < QB_NF; ++f) asm volatile("" ::"v"(wa[f]));
+  int chunk = 0;
+  bool dead = false;
+  auto run = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    auto kstep = [&](f32x4 (&acc)[4], int kk) {
+      const chunk16 hf = hfrag(kk);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = mfma_chunk<bf16>(wa[g * 8 + kk], hf, acc[g]);
+    };
+    auto step = [&](const int t, u32x4 (&gc)[2], u32x4 (&go)[2]) {
+      stamp(t, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t >= 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // gc (gx of step t) landed
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 v4 = gc[g >> 1];
+        const bf16x4 v = __builtin_bit_cast(bf16x4, (g & 1) ? u32x2{v4[2], v4[3]} : u32x2{v4[0], v4[1]});
+        acc[g] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      }
+      stamp(t, 1);
+      const int par = (t - 1) & 1;
+      u32x4 xv[3];
+      if (t > 0) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) poll(xv[p], xoff((Q + 1 + p) & 3, par));
+      }
+      gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);  // gx of step t+2 into the slot just consumed
+      kstep(acc, 2 * Q);
+      kstep(acc, 2 * Q + 1);
+      stamp(t, 2);
+      if (t > 0) {
+        __builtin_amdgcn_sched_barrier(0);  // the own-unit MFMAs stay ahead of the waits
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // P landed (G may still be in flight)
+        const uint32_t want = tag_base + (uint32_t)(t - 1);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          uint64_t t0 = 0;
+          while (!dead && !__all(xv[p][1] == want && xv[p][3] == want)) {
+            if (!t0) {
+              t0 = __builtin_amdgcn_s_memrealtime();
+            } else if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+              if (sync.error && lane == 0) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              dead = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_waitcnt vmcnt(0)" : "=v"(xv[p])
+                         : "v"(xoff((Q + 1 + p) & 3, par)), "s"(xr) : "memory");
+          }
+          hput(64 * ((Q + 1 + p) & 3) + 16 * w + 4 * (lane >> 4), u32x2{xv[p][0], xv[p][2]});
+        }
+      }
+      stamp(t, 3);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B1: the partners' units of h_{t-1}
+      if constexpr (Q != 0) { kstep(acc, 0); kstep(acc, 1); }
+      if constexpr (Q != 1) { kstep(acc, 2); kstep(acc, 3); }
+      if constexpr (Q != 2) { kstep(acc, 4); kstep(acc, 5); }
+      if constexpr (Q != 3) { kstep(acc, 6); kstep(acc, 7); }
+      float hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lstm_cell<true>(acc, r, c[r], hv[r]);
+      const u32x2 hp = pack_bf16x4(hv[0], hv[1], hv[2], hv[3]);
+      const uint32_t tag = tag_base + (uint32_t)t;
+      const u32x4 xo = {hp[0], tag, hp[1], tag};
+      // (the s_nops: a VALU write of a store's data VGPRs right after a dwordx3/x4 store is a hazard the
+      // compiler does not see through inline asm)
+      if (xl2)  // the whole quad on one XCD: the exchange stays in that XCD's L2
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(xo), "v"(xoff(Q, t & 1)), "s"(xr)
+                     : "memory");
+      else  // write-through
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1\n\ts_nop 2" ::"v"(xo), "v"(xoff(Q, t & 1)), "s"(xr)
+                     : "memory");
+      asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 2" ::"v"(hp), "v"(o_lane + (uint32_t)t * (HD * 2)),
+                   "s"(orsc) : "memory");
+      hput(u0, hp);  // own units of h_t (the own-unit reads of this step retired before B1)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B2: own h_t visible to every wave
+      stamp(t, 4);
+      if (sync.time_mode && chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) {
+        // end of a time chunk: publish its h rows, then wait for the next chunk's gate projection
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int c0 = chunk;
+        while (chunk < sync.nr && t + 1 >= sync.seq_end[chunk]) ++chunk;
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          for (int cc = c0; cc < chunk; ++cc)
+            __hip_atomic_fetch_add(sync.done + cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (chunk < sync.nr) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(sync.ready + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sync.epoch) {
+              __builtin_amdgcn_s_sleep(8);
+              if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+                if (sync.error) __hip_atomic_store(sync.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+              }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        if (chunk < sync.nr) {  // rows t+1 and t+2 may have been prefetched before the hand-off: reload
+          __syncthreads();
+          gload(go, t + 1 < Tn ? t + 1 : Tn - 1);
+          gload(gc, t + 2 < Tn ? t + 2 : Tn - 1);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+    };
+    for (int t = 0; t < Tn; t += 2) {
+      step(t, ga, gb);
+      if (t + 1 < Tn) step(t + 1, gb, ga);
+    }
+  };
+  switch (q) {
+    case 0: run(std::integral_constant<int, 0>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 3>{}); break;
+  }
+  if constexpr (ST) {
+    if (samp && Tn >= sync.stamp_t0 + 4)
+      for (int i = 0; i < 20; ++i) g_lstm_stamps[blockIdx.x][i / 5][i % 5] = stl[i];
+  }
+  if (sync.ready && !sync.time_mode) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = ra; r <= rb; ++r) __hip_atomic_fetch_add(sync.done + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------
 // fp32 parity mode: W_hh split over a QUAD of workgroups, products on split-bf16 operands.
 //
 // The fp32 recurrence on v_mfma_f32_16x16x4_f32 (lstm_kernel<float>) streams W_hh from L2 at one CU
@@ -1061,11 +1346,11 @@ hipError_t launch_lstm_resident(const bf16* gx, int S, int Tn, const bf16* whh_p
   return hipGetLastError();
 }
 size_t lstm_pair_xbuf_bytes(int S) { return (size_t)((S + NS - 1) / NS) * P_SLOT * 16; }
-int lstm_pair_workgroups(int S) { return 2 * ((S + NS - 1) / NS); }
+int lstm_pair_workgroups(int S, int quad) { return (quad ? 4 : 2) * ((S + NS - 1) / NS); }
 
 hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out,
                             int64_t out_seq_stride, hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag,
-                            int xplain) {
+                            int xplain, int quad) {
   if (S <= 0 || Tn <= 0 || seq0 < 0 || !xbuf || xtag == 0 || (uint64_t)xtag + (uint64_t)Tn > 0xFFFFFFFFull)
     return hipErrorInvalidValue;
   LstmSync sy{};
@@ -1084,8 +1369,21 @@ hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16*
   static const int st0 = getenv("VAP_LSTM_STAMP_T0") ? atoi(getenv("VAP_LSTM_STAMP_T0")) : 100;
   sy.stamp_t0 = st0;
   const int groups = (S + NS - 1) / NS;
-  const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
   static const bool stamps = getenv("VAP_LSTM_STAMPS") != nullptr;
+  if (quad) {  // quads (b, b+8, b+16, b+24) of every 32 blocks; padding quads exit
+    const dim3 gq(32 * ((groups + 7) / 8));
+    // 96 KiB of (unused) dynamic LDS: one quarter per CU (its 4 waves hold half the register file, so two
+    // quarters could otherwise share the SIMDs, and the persistent conv launches budget whole CUs for it)
+    constexpr size_t excl = 96 * 1024;
+    if (stamps)
+      hipLaunchKernelGGL((lstm_quadb_kernel<true>), gq, dim3(256), excl, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
+                         out_seq_stride, sy, (u32x4*)xbuf);
+    else
+      hipLaunchKernelGGL((lstm_quadb_kernel<false>), gq, dim3(256), excl, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
+                         out_seq_stride, sy, (u32x4*)xbuf);
+    return hipGetLastError();
+  }
+  const dim3 grid(16 * ((groups + 7) / 8));  // pairs (b, b + 8) of every 16 blocks; padding pairs exit
   if (stamps)
     hipLaunchKernelGGL((lstm_pair_kernel<true, true>), grid, dim3(512), 0, st, gx, seq0, S, Tn, (const chunk16*)whh_pair, out,
                        out_seq_stride, sy, (u32x4*)xbuf);

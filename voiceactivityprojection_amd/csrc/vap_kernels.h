@@ -145,7 +145,7 @@ hipError_t launch_pack_whh_resident(const float* whh, bf16* packed, hipStream_t 
 // gx: the pair-layout gate buffer (gx_pair_block) whose sequence seq0 is this launch's sequence 0
 hipError_t launch_lstm_pair(const bf16* gx, int seq0, int S, int Tn, const bf16* whh_pair, bf16* out, int64_t out_seq_stride,
                             hipStream_t st, const LstmSync* sync, void* xbuf, unsigned xtag,
-                            int xplain = 0);
+                            int xplain = 0, int quad = 0);
 hipError_t launch_pack_whh_pair(const float* whh, bf16* packed, hipStream_t st);
 size_t lstm_pair_xbuf_bytes(int S);
 // fp32 parity mode: W_hh split over a QUAD of workgroups (k_lstm.hip lstm_quad_kernel), split-bf16 products:
@@ -176,7 +176,9 @@ inline int64_t gx_pair_elems(int S, int64_t Tn) { return (int64_t)((S + 15) / 16
 __host__ __device__ inline int gx_wrow(int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); }
 // [S][Tn][1024] natural gate order -> the pair layout (kernel tests)
 hipError_t launch_pack_gx_pair(const bf16* in, bf16* out, int S, int Tn, hipStream_t st);
-int lstm_pair_workgroups(int S);
+// workgroups of one launch_lstm_pair launch (each publishes the done counters): 2 per 16 sequences, 4 with quad
+// (lstm_quadb_kernel: the same packed W_hh, gate layout and exchange buffer)
+int lstm_pair_workgroups(int S, int quad = 0);
 hipError_t launch_scale_gates(const bf16* in, bf16* out, int64_t n, hipStream_t st);
 hipError_t launch_pack_wih_prescaled(const float* wih, bf16* packed, const float* bih, const float* bhh, float* bias,
                                      hipStream_t st);

@@ -107,8 +107,9 @@ int vap_test_attention(int precision, const void* Q, int64_t q_ld, int64_t q_seq
 }
 
 // gx: [S][T][1024] storage type for bf16 (the engine's resident kernel) / fp32 for fp32;
-// variant 1 = the L2-streaming bf16 kernel (fp32 gx).  whh_packed: scratch of 1024*256 storage
-// elements; out: [S][T][256] storage type.
+// variant 1 = the L2-streaming bf16 kernel (fp32 gx), 2 the single-CU resident kernel, 3 the pair split,
+// 5 the quad split (bf16), 4 the fp32 quad split on split-bf16 operands.  whh_packed: scratch of
+// 1024*256 storage elements; out: [S][T][256] storage type.
 int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh, void* whh_packed, void* out,
                   int variant, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -125,7 +126,8 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
     (void)hipFree(gs);
     return rc_of(e);
   }
-  if (precision == VAP_PRECISION_BF16 && variant == 3) {  // the pair split (lstm_pair_kernel), pre-scaled
+  if (precision == VAP_PRECISION_BF16 && (variant == 3 || variant == 5)) {  // pair split (lstm_pair_kernel) / quad
+                                                                             // split (lstm_quadb_kernel), pre-scaled
     void* gs = nullptr;
     void* xb = nullptr;
     const int64_t n = (int64_t)S * T * 1024;
@@ -145,7 +147,7 @@ int vap_test_lstm(int precision, const void* gx, int S, int T, const float* whh,
     if (e == hipSuccess) e = launch_pack_gx_pair((const bf16*)gs, (bf16*)gp, S, T, st);  // the engine's layout
     if (e == hipSuccess)
       e = launch_lstm_pair((const bf16*)gp, 0, S, T, (const bf16*)whh_packed, (bf16*)out, (int64_t)T * 256, st, nullptr,
-                           xb, 1);
+                           xb, 1, 0, variant == 5 ? 1 : 0);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (gp) (void)hipFree(gp);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
