@@ -40,7 +40,10 @@ __device__ unsigned long long g_g2_stamps[8][2][4][6];
 // done, [3] epilogue math done, [4] stores issued, [5] stores complete
 __device__ unsigned long long g_g2_tile[8][6];
 
-template <typename TOut, bool ST = false>
+// ACT = g.act as a template parameter: a runtime branch between the activations over the 128 live
+// accumulator registers made the compiler copy all of them at the merge and spill (scratch in the
+// epilogue: 148-180 B per lane, written and read back once per tile)
+template <typename TOut, bool ST, int ACT>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -267,14 +270,14 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(GemmArgs g) {
       for (int i = 0; i < 8; ++i) acc[j][i] = (acc[j][i] - mean[i]) * rstd[i] * ga + be;
     }
   }
-  if (g.act == 1) {
+  if constexpr (ACT == 1) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[j][i][r] = fmaxf(acc[j][i][r], 0.f);
-  } else if (g.act == 2) {
+  } else if constexpr (ACT == 2) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -352,10 +355,15 @@ hipError_t launch_gemm2(const GemmArgs& g, hipStream_t st) {
   const int mtiles = g.c_pair ? (g.n_seq + 15) / 16 * ((g.M_per_seq + 15) / 16) : (M + BM - 1) / BM;
   const dim3 grid((unsigned)((mtiles + 7) / 8 * 8 * (g.N / BN)));  // XCD-aware 1-D order (see the kernel)
   static const bool stamps = getenv("VAP_GEMM2_STAMPS") != nullptr;
-  if (stamps)
-    hipLaunchKernelGGL((gemm2_kernel<TOut, true>), grid, dim3(512), 0, st, g);
-  else
-    hipLaunchKernelGGL((gemm2_kernel<TOut, false>), grid, dim3(512), 0, st, g);
+  if (g.act < 0 || g.act > 2) return hipErrorInvalidValue;
+  auto go = [&](auto stc) {
+    constexpr bool S_ = decltype(stc)::value;
+    if (g.act == 1) hipLaunchKernelGGL((gemm2_kernel<TOut, S_, 1>), grid, dim3(512), 0, st, g);
+    else if (g.act == 2) hipLaunchKernelGGL((gemm2_kernel<TOut, S_, 2>), grid, dim3(512), 0, st, g);
+    else hipLaunchKernelGGL((gemm2_kernel<TOut, S_, 0>), grid, dim3(512), 0, st, g);
+  };
+  if (stamps) go(std::true_type{});
+  else go(std::false_type{});
   return hipGetLastError();
 }
 
