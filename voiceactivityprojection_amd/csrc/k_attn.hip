@@ -322,11 +322,14 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
         for (int k = 0; k < 4; ++k) st[t] = mfma32(*(const chunk16*)(Kt + t * 32 * TROW + koff[k]), qf[k], st[t]);
       }
       if (key0 + KB2 - 1 > qw0) {  // wave-uniform: a diagonal tile
+        // register (t, r) holds key key0 + 4 hl + 32t + 8(r>>2) + (r&3): one compare against an inline
+        // constant per register
+        const int dd = qv - key0 - 4 * hl;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (key0 + 32 * t + 8 * (r >> 2) + 4 * hl + (r & 3) > qv) st[t][r] = -INFINITY;
+            if (32 * t + 8 * (r >> 2) + (r & 3) > dd) st[t][r] = -INFINITY;
       }
       float b0 = st[0][0], b1 = st[1][0];
 #pragma unroll
