@@ -28,14 +28,7 @@
 #include "vap_common.h"
 #include "vap_kernels.h"
 
-#ifndef VAP_BLK_NT
-#define VAP_BLK_NT 0  // A/B builds: 1 = the O panel / residual-row loads of the row kernels as non-temporal
-#endif
 namespace {
-// streaming operand loads of the row kernels (O panel, residual rows): read once per launch
-VAP_DEV chunk16 buf_load16s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(chunk16, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, VAP_BLK_NT ? 2 : 0));
-}
 
 constexpr int D = 256;
 constexpr int ROWB = D * 2;  // bf16 row of the panel / of a hidden slice: 512 B = 32 chunks
@@ -224,7 +217,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     uint32_t oo[OPT];
     rows16(m0 + (tid >> 5), g.o_seq, obase, 2, oo, OPT);
 #pragma unroll
-    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16s(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
   }
   // lane's rows j*16 + l16 of x (recomputed for the stores at the end, not held live)
   const int64_t xbase = roff(m0, g.x_seq);
@@ -237,7 +230,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4 v = __builtin_bit_cast(f32x4, buf_load16s(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
+        const f32x4 v = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
         if constexpr (OPROJ) {
           xt[i][j] = v;
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -559,7 +552,7 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
     uint32_t oo[OPT];
     rows16_off(m0 + (tid >> 5), g.M, rps, g.o_seq, D, obase, 2, oo, OPT);
 #pragma unroll
-    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16s(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
   }
   const int64_t xbase = roff(m0, g.x_seq, D);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.x + xbase, 0x7FFFFFF0u);
@@ -572,7 +565,7 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
   for (int j = 0; j < MT; ++j)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      acc[i][j] = __builtin_bit_cast(f32x4, buf_load16s(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
+      acc[i][j] = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
 
   // weights through buffer resources (see block_kernel)
   const __amdgpu_buffer_rsrc_t rWo = make_rsrc(g.Wo, 0x7FFFFFF0u), rWp = make_rsrc(g.Wp, 0x7FFFFFF0u),

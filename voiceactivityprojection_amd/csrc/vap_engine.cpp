@@ -17,10 +17,6 @@
 #include "vap_common.h"
 #include "vap_kernels.h"
 
-#ifndef VAP_DOWN_SMALL
-#define VAP_DOWN_SMALL 0  // A/B builds: the time-chunked downsample on 128-row gemm_kernel tiles
-#endif
-
 namespace {
 
 thread_local std::string g_err;
@@ -1409,7 +1405,6 @@ int tc_back_end(vap_handle* h, const Plan& p, const TcSched& t, const LstmSync& 
       ga.act = 2;
       ga.gamma = h->P("encoder.downsample.2.ln.weight");
       ga.beta = h->P("encoder.downsample.2.ln.bias");
-      ga.small_tiles = VAP_DOWN_SMALL;
       HIPCHK(hgemm<T>(h, ga, bs, true));
     }
     // per-chunk heads need the final x as bf16 from the last layer's fused block kernel
