@@ -452,15 +452,16 @@ def fixture_errors(out, B: int, seconds: float, precision: str):
 
 
 def _leg(model, wav, steps: int, warmup: int, keys=None):
-    """Steps of model.probs on a resident batch: (ms per step, outputs of the last step)."""
-    out = None
-    for _ in range(warmup):
-        out = model.probs(wav)
+    """Steps of model.probs on a resident batch: (ms per step, outputs of the last step).  Like the
+    headline loop, every step writes into the same preallocated outputs (the first warm-up step's)."""
+    out = model.probs(wav)
+    for _ in range(warmup - 1):
+        model.probs(wav, out=out)
     torch.cuda.synchronize()
     model.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        out = model.probs(wav)
+        model.probs(wav, out=out)
     torch.cuda.synchronize()
     model.synchronize()
     return (time.perf_counter() - t0) / steps * 1e3, out
