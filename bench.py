@@ -484,6 +484,12 @@ def extras(args, model, dev, sd_np, steps: int = 5, warmup: int = 3):
                            "1 GPU, VapGPT.probs"}
     del wav4
     if args.precision != "fp32":
+        # the headline model's native handle goes first: its side streams would otherwise share the
+        # process's GPU_MAX_HW_QUEUES (4) hardware queues with the fp32 model's, and a persistent
+        # recurrence queued on the caller stream's hardware queue serialises the leg (measured 14 %
+        # slower than the same mode alone: 43.8k vs 49.9k audio-s/s, profiles/r4/bench_s9.json)
+        model._free_handle()
+        torch.cuda.synchronize()
         B, n = args.batch, int(args.seconds * 16000)
         m32 = VapGPT(precision="fp32")
         m32.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
