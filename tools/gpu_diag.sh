@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-diag}
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in default $LIBS; do
     if [ $lib = default ]; then e="VAP_AB_DEFAULT=1"; else e="VAP_LIB_AB=$lib"; fi
     env $e timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras --steps 10 > gpurun_out/${TAG}_${lib}_$r.json 2>gpurun_out/${TAG}_${lib}_$r.err || { tail -20 gpurun_out/${TAG}_${lib}_$r.err; exit 1; }

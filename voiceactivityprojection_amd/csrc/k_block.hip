@@ -64,6 +64,14 @@ VAP_DEV void panel_put(unsigned char* img, int row, int w, int lg, u32x2 a, u32x
   *(u32x4*)(img + row * ROWB + xswz(row, c) * 16) = u32x4{a[0], a[1], b[0], b[1]};
 }
 
+// the residual rows' stores: write-through (sc1) by default; A/B builds: BLK_XST 1 plain, 2 nt
+#ifndef BLK_XST
+#define BLK_XST 0
+#endif
+VAP_DEV void xstore(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, BLK_XST == 0 ? 16 : BLK_XST == 1 ? 0 : 2);
+}
+
 // GELU in sigmoid form, x * sigmoid(-x (c1 + c2 x^2) ln 2), with c1 / c2 fitted to the erf GELU
 // (max |error| 2.7e-4 over the reals, below half a bf16 ulp for |x| >= 0.14): one v_exp + one v_rcp
 // + 5 VALU.  Large negative x: exp2 -> +inf, rcp -> 0, result -0; large positive: x.
@@ -172,6 +180,11 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   constexpr int Q2 = Q0 + 48;            // first k-step of the fused next-layer projections
   constexpr int NQ = Q2 + 8 * (NP2 + NR2);  // Wo 8 + 3 x (W1 8 + W2 8) [+ Wp / Wr 8 per N tile]
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+#ifndef BLK_DIAG
+#define BLK_DIAG 0
+#endif
+  // diagnostics (A/B builds only, outputs not meaningful): 1 no weight refills, 2 no GELU,
+  // 4 A fragments read once per pass, 8 no O / x loads, 16 no stores
   unsigned char* P = smem;
   unsigned char* H = smem + C::OFF_H;
   float* red0 = (float*)(smem + C::OFF_RED);
@@ -217,7 +230,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     uint32_t oo[OPT];
     rows16(m0 + (tid >> 5), g.o_seq, obase, 2, oo, OPT);
 #pragma unroll
-    for (int k = 0; k < OPT; ++k) ot[k] = buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
+    for (int k = 0; k < OPT; ++k) ot[k] = (BLK_DIAG & 8) ? chunk16{0u, 0u, 0u, 0u} : buf_load16(ro, oo[k] + (uint32_t)(tid & 31) * 16u, 0);
   }
   // lane's rows j*16 + l16 of x (recomputed for the stores at the end, not held live)
   const int64_t xbase = roff(m0, g.x_seq);
@@ -230,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4 v = __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
+        const f32x4 v = (BLK_DIAG & 8) ? f32x4{0.f, 0.f, 0.f, 0.f} : __builtin_bit_cast(f32x4, buf_load16(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, 0));
         if constexpr (OPROJ) {
           xt[i][j] = v;
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -274,10 +287,14 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
   // fragment j of k-step ks sits at byte (j*16 + l16) * 512 + ((ks*4 + lg) ^ l16) * 16 = abase(j) ^ ks*64
   // (ks*4 only touches chunk bits 2..4 and lg the low two, so the XOR splits)
   const uint32_t afo = (uint32_t)(l16 * ROWB + (lg ^ l16) * 16);
+  chunk16 afk[MT];
   auto kstep = [&](const unsigned char* img, int ks, int q, f32x4 (&c)[2][MT]) {
     chunk16 af[MT];
 #pragma unroll
-    for (int j = 0; j < MT; ++j) af[j] = *(const chunk16*)(img + j * 16 * ROWB + (afo ^ (uint32_t)(ks * 64)));
+    for (int j = 0; j < MT; ++j) {
+      if (!(BLK_DIAG & 4) || ks == 0) afk[j] = *(const chunk16*)(img + j * 16 * ROWB + (afo ^ (uint32_t)(ks * 64)));
+      af[j] = afk[j];
+    }
     chunk16* wf = wr[q % NPF];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -285,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
       for (int j = 0; j < MT; ++j) c[i][j] = mfma_chunk<bf16>(wf[i], af[j], c[i][j]);
     // unconditional refill (the tail reloads the last step): a conditional load makes the
     // compiler's vmcnt bookkeeping drain the whole prefetch
-    wload(q + NPF < NQ ? q + NPF : NQ - 1, wf);
+    if (!(BLK_DIAG & 1)) wload(q + NPF < NQ ? q + NPF : NQ - 1, wf);
     // keep k-steps apart: left alone, the scheduler hoists later k-steps' fragment reads over
     // earlier MFMAs and spills (the other wave on the SIMD covers the read latency instead)
     __builtin_amdgcn_sched_barrier(0);
@@ -332,7 +349,8 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j)
-        hb[i][j] = pack_bf16x4(gelu_sig(up[i][j][0]), gelu_sig(up[i][j][1]), gelu_sig(up[i][j][2]),
+        hb[i][j] = (BLK_DIAG & 2) ? pack_bf16x4(up[i][j][0], up[i][j][1], up[i][j][2], up[i][j][3])
+                                  : pack_bf16x4(gelu_sig(up[i][j][0]), gelu_sig(up[i][j][1]), gelu_sig(up[i][j][2]),
                                gelu_sig(up[i][j][3]));
     __syncthreads();  // every wave is done reading H (the O panel / the previous slice)
     stamp(5 + 4 * s);
@@ -355,7 +373,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+        if (!(BLK_DIAG & 16)) xstore(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
     if (g.xb) {  // bf16 copy (the combinator's input after the last layer): same rows, half the bytes
       const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.xb + xbase, 0x7FFFFFF0u);
 #pragma unroll
@@ -427,7 +445,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
           a[d] = sw[0];
           b[d] = sw[1];
         }
-        buf_store16(rc, co[j] + col * 2u, u32x4{a[0], a[1], b[0], b[1]});
+        if (!(BLK_DIAG & 16)) buf_store16(rc, co[j] + col * 2u, u32x4{a[0], a[1], b[0], b[1]});
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -620,7 +638,7 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+        xstore(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
   }
   if constexpr (NR > 0) {  // raw rows (bf16) -> H
 #pragma unroll

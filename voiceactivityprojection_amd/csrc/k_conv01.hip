@@ -291,14 +291,18 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
   stamp();
 
   // unit u (slot u % 3 = SL, a compile-time constant so every LDS offset is an immediate)
-  auto unit = [&](const int u, auto slc, chunk16* wf, chunk16* wn1, const bool last1, const bool nosl) {
+#ifndef C01_DIAG
+#define C01_DIAG 0
+#endif
+  auto unit = [&](const int u, auto slc, chunk16* wf, chunk16* wn1, const bool last1, const bool nosl_) {
     constexpr int SL = decltype(slc)::value;
+    const bool nosl = nosl_ || (C01_DIAG & 1);  // diag 1: no slice production
     // B_u: own slice u+1 stores retired; W1 of unit u (issued one unit ago) landed
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((C01_DIAG & 2) == 0) __builtin_amdgcn_s_barrier();  // diag 2: no unit barrier
     __builtin_amdgcn_sched_barrier(0);
-    if (!last1) wload(u + 1, wn1);
+    if (!last1 && (C01_DIAG & 8) == 0) wload(u + 1, wn1);  // diag 8: no W1 refill
     const int v = u + 2;
     chunk16 c0, sv;
     f32x4 bt, z;
@@ -316,8 +320,10 @@ __global__ __launch_bounds__(512, 1) void conv01m_kernel(const float* __restrict
         if (n == 31) pstore(std::integral_constant<int, (SL + 2) % 3>{}, v, 4, z);
       }
       mfma32_acc(acc[n & 7], wf[n >> 3], gf[n % (GA + 1)]);
-      if (n + GA < 32) gf[(n + GA) % (GA + 1)] = gread(slc, n + GA);
-      else if (!last1) gf[(n + GA) % (GA + 1)] = gread(std::integral_constant<int, (SL + 1) % 3>{}, n + GA - 32);
+      if constexpr ((C01_DIAG & 4) == 0) {  // diag 4: G fragments re-used (no LDS reads)
+        if (n + GA < 32) gf[(n + GA) % (GA + 1)] = gread(slc, n + GA);
+        else if (!last1) gf[(n + GA) % (GA + 1)] = gread(std::integral_constant<int, (SL + 1) % 3>{}, n + GA - 32);
+      }
     }
     if ((u & 7) == 7) stamp();
   };
