@@ -222,9 +222,6 @@ VAP_DEV float xmax2(float v) {  // max with lane ^ 32
   return fmaxf(a, b);
 }
 
-#ifndef ATT_VSUM
-#define ATT_VSUM 0  // A/B: row sums by fp32 VALU adds of the unrounded p instead of a ones-row MFMA
-#endif
 #ifndef ATT_DIAG
 #define ATT_DIAG 0  // diagnostics (A/B builds only, outputs not meaningful): 1 no exp, 2 no row-sum MFMA, 4 K/V tile 0 only
 #endif
@@ -278,7 +275,6 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
 
   float m = -INFINITY;  // running max of the true log2 scores
   f32x16 o0 = {}, o1 = {}, ls = {};
-  float lsum = 0.f;  // ATT_VSUM: the lane's partial row sum (its 32 keys of each tile), fp32 VALU adds
   const bf16x8 ones8 = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const chunk16 ones = __builtin_bit_cast(chunk16, ones8);
 
@@ -352,8 +348,7 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
         m = mn;
         o0 *= alpha;
         o1 *= alpha;
-        if constexpr (ATT_VSUM) lsum *= alpha;
-        else ls *= alpha;
+        ls *= alpha;
       }
       const float m0 = m - tofs, m1 = m0 - off32;
       bf16x8 pb[2][2];
@@ -363,11 +358,8 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
         for (int k = 0; k < 2; ++k) {
           const float mt = t ? m1 : m0;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float pe = (ATT_DIAG & 1) ? st[t][8 * k + e] - mt : __builtin_amdgcn_exp2f(st[t][8 * k + e] - mt);
-            pb[t][k][e] = (bf16)pe;
-            if constexpr (ATT_VSUM) lsum += pe;
-          }
+          for (int e = 0; e < 8; ++e)
+            pb[t][k][e] = (ATT_DIAG & 1) ? (bf16)(st[t][8 * k + e] - mt) : (bf16)__builtin_amdgcn_exp2f(st[t][8 * k + e] - mt);
         }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -383,7 +375,7 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
             if (u == 0) o0 = mfma32(vf, p, o0);
             else o1 = mfma32(vf, p, o1);
           }
-          if (!(ATT_DIAG & 2) && !ATT_VSUM) ls = mfma32(ones, p, ls);
+          if (!(ATT_DIAG & 2)) ls = mfma32(ones, p, ls);
         }
     }
     if (!(ATT_DIAG & 4) && kb + 1 < nkb) lstore(cur ^ 1);
@@ -398,13 +390,7 @@ __global__ __launch_bounds__(256, 3) void attn4_kernel(AttnArgs a, int nqb, int 
     if (kb + 1 < nkb) tile(kb + 1, std::integral_constant<int, 1>{});
   }
   // O^T: lane holds its query's dims 32u + 8g + 4hl + e in register 4g + e of o_u
-  float lt = ls[0];
-  if constexpr (ATT_VSUM) {  // the query's other 32 keys of every tile sit in lane ^ 32
-    float a = lsum, b2 = lsum;
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b2));
-    lt = a + b2;
-  }
-  const float inv = 1.0f / lt;
+  const float inv = 1.0f / ls[0];
   if (qv < a.T) {
     bf16* orow = (bf16*)a.O + (int64_t)s * a.o_seq + (int64_t)qv * a.o_ld + h * HDIM;
 #pragma unroll

@@ -64,14 +64,6 @@ VAP_DEV void panel_put(unsigned char* img, int row, int w, int lg, u32x2 a, u32x
   *(u32x4*)(img + row * ROWB + xswz(row, c) * 16) = u32x4{a[0], a[1], b[0], b[1]};
 }
 
-// the residual rows' stores: write-through (sc1) by default; A/B builds: BLK_XST 1 plain, 2 nt
-#ifndef BLK_XST
-#define BLK_XST 0
-#endif
-VAP_DEV void xstore(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, BLK_XST == 0 ? 16 : BLK_XST == 1 ? 0 : 2);
-}
-
 // GELU in sigmoid form, x * sigmoid(-x (c1 + c2 x^2) ln 2), with c1 / c2 fitted to the erf GELU
 // (max |error| 2.7e-4 over the reals, below half a bf16 ulp for |x| >= 0.14): one v_exp + one v_rcp
 // + 5 VALU.  Large negative x: exp2 -> +inf, rcp -> 0, result -0; large positive: x.
@@ -373,7 +365,7 @@ __global__ __launch_bounds__(512, 1) void block_kernel(BlockArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        if (!(BLK_DIAG & 16)) xstore(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+        if (!(BLK_DIAG & 16)) buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
     if (g.xb) {  // bf16 copy (the combinator's input after the last layer): same rows, half the bytes
       const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.xb + xbase, 0x7FFFFFF0u);
 #pragma unroll
@@ -638,7 +630,7 @@ __global__ __launch_bounds__(512, 1) void lnproj_kernel(LnProjArgs g) {
     for (int j = 0; j < MT; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        xstore(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
+        buf_store16_wt(rx, xo[j] + (uint32_t)(w * 32 + i * 16 + lg * 4) * 4u, __builtin_bit_cast(u32x4, acc[i][j]));
   }
   if constexpr (NR > 0) {  // raw rows (bf16) -> H
 #pragma unroll
