@@ -380,12 +380,12 @@ def run_rank(args) -> int:
             # by tools/pmc_traffic.sh on the serial schedule: PMC windows of overlapped kernels are polluted
             # by the concurrent LSTM) x the rows of one launch here
             traffic, traffic_src = None, None
-            tp = os.path.join(REPO, "profiles", "r3_traffic_pmc.json")  # the current conv01 kernel (v11)
+            tp = os.path.join(REPO, "profiles", "r4", "traffic_pmc_s6.json")  # the current conv01 kernel (round 4, session 6)
             if dominant == "conv1" and args.precision == "bf16" and os.path.exists(tp):
                 per_row = json.load(open(tp))["conv1"]["hbm_bytes_per_row"]
                 rows_per_launch = 2 * B * L[1] / launches_per_step
                 traffic = round(per_row * rows_per_launch / 1e9, 3)
-                traffic_src = "profiles/r3_traffic_pmc.json (GB per launch)"
+                traffic_src = "profiles/r4/traffic_pmc_s6.json (GB per launch)"
             line["roofline"] = {"kernel": dominant, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                                 "traffic_source": traffic_src, "flop_per_launch": flop_per_launch,
