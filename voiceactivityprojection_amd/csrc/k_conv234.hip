@@ -400,6 +400,257 @@ __global__ __launch_bounds__(512, 1) void convk4_kernel(ConvK4Args a, int ntb, i
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// convk4h_kernel (production since round 4, session 6): 128-row tiles on 4 waves, two workgroups per CU.
+// The 256-row kernel above holds a whole CU (124 KiB LDS, 8 waves x 256 registers), so its prologue
+// and its epilogue (ChannelNorm exchange, stores and their drain: ~25k of ~72k cycles per tile) leave
+// the matrix pipes idle.  Here a workgroup owns 128 output rows and 4 waves, wave w all 128 rows of
+// output channels 64w .. 64w+63 (2 channel tiles x 4 row tiles of v_mfma_f32_32x32x16_bf16, 128
+// accumulators in AGPRs), 62 KiB of LDS: two workgroups share a CU (one wave of each per SIMD), so one
+// workgroup's prologue / epilogue runs beside the other's MFMAs.  Each G fragment read from LDS feeds
+// two MFMAs (the two channel tiles); W comes from L2 into ONE register set of 16 fragments, each
+// refilled with the next block's fragment right after its last MFMA (a block of slack).  Per block
+// and wave the vector-memory issue order is fixed -- step f: W refill f (2 loads), then DMA piece f
+// of block CB+2 for f < 5 -- so "W(CB)[f] landed" is vmcnt(19) before step f in every block but the
+// last (whose step-f waits are a table), and the block barrier after that wait also covers DMA(CB).
+// Blocks 6 and 7 DMA nothing real: 6 re-issues block 7's pieces into slot 2 (unused by then) to keep
+// the count uniform, 7 issues no loads at all.
+// ------------------------------------------------------------------------------------------------
+constexpr int CH_HR = 144;                 // half-rows per parity half (>= 129)
+constexpr int CH_HALF = CH_HR * 64;        // 9216 B
+constexpr int CH_SLAB = 2 * CH_HALF;       // 18432 B
+constexpr int CH_PIECES = 2 * (CH_HR / 16);  // 18 DMA pieces of 1 KiB per slab
+constexpr int CH_RED = 3 * CH_SLAB;        // 55296: [128 rows][8 groups of 32 channels] (mean, M2)
+constexpr int CH_PAR = CH_RED + 128 * 8 * 8;  // 63488: bias | gamma | beta
+constexpr int CH_LDS = CH_PAR + 3 * 256 * 4;  // 66560 B
+
+__global__ __launch_bounds__(256, 2) void convk4h_kernel(ConvK4Args a, int ntb) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[CH_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 64w .. 64w+63
+  const int s = blockIdx.x / ntb, t0 = (blockIdx.x - s * ntb) * 128;
+  if (tid < 192) {
+    const float* src = tid < 64 ? a.bias : (tid < 128 ? a.gamma : a.beta);
+    ((f32x4*)(smem + CH_PAR))[tid] = ((const f32x4*)src)[tid & 63];
+  }
+  const bf16* in = a.in + (int64_t)s * a.in_seq_stride;
+  const __amdgpu_buffer_rsrc_t crs =
+      make_rsrc(in + (int64_t)2 * t0 * 256, (uint32_t)max(0, a.in_rows - 2 * t0) * 512u);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  // DMA piece k (0..4) of block cb into slot sl: piece q = w + 4k (waves 2, 3 repeat piece 14 / 15 as
+  // their fifth); half hb = q / 9, half-rows 16p .. of it; lane -> half-row lane >> 2, swizzled chunk
+  auto dlane = [&]() -> uint32_t {
+    const int ln = ck_lane();
+    return (uint32_t)((ln >> 2) * 1024 + (((ln & 3) - (ln >> 4)) & 3) * 16);
+  };
+  auto dma1 = [&](uint32_t dl, int cb, int sl, int k) {
+    const int q = (k == 4 && w >= 2) ? w + 12 : w + 4 * k;
+    const int hb = q >= CH_PIECES / 2, p = q - hb * (CH_PIECES / 2);
+    const uint32_t po = __builtin_amdgcn_readfirstlane((uint32_t)(((32 * p + hb) * 256 + cb * 32) * 2));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(sl * CH_SLAB + hb * CH_HALF + p * 1024));
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(dl + po), "s"(crs), "s"(dst) : "memory");
+  };
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.W, 32 * 256 * 64);
+  // W fragment (f = 2 tap + k half, channel tile c) of block cb: channel 64w + 32c + lane % 32
+  // the lane part of a W fragment's offset (channel tile 1 = + 32 channels x 64 B), rebuilt per block
+  auto wlane = [&]() -> uint32_t {
+    const int ln = ck_lane();
+    return (uint32_t)((w * 64 + (ln & 31)) * 64 + (ln >> 5) * 16);
+  };
+  auto wload = [&](uint32_t wlo, int cb, int f, int c, chunk16& wf) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(wf)
+                 : "v"(wlo), "s"(wrs), "s"(((f >> 1) * 8 + cb) * 16384 + (f & 1) * 32 + c * 32 * 64) : "memory");
+  };
+  chunk16 W[8][2];
+  {
+    const uint32_t wlo = wlane(), dl = dlane();
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) wload(wlo, 0, f, c, W[f][c]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dma1(dl, 0, 0, k);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dma1(dl, 1, 1, k);
+  }
+
+  __syncthreads();  // parameters in LDS
+  const float* PR = (const float*)(smem + CH_PAR);
+  f32x16 acc[2][4];
+  {
+    const int ln = ck_lane();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 bb[4];
+      const int c0 = w * 64 + c * 32 + 4 * (ln >> 5);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bb[q] = *(const f32x4*)(PR + c0 + 8 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[c][r][e] = bb[e >> 2][e & 3];
+    }
+    asm volatile("s_nop 4" : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]));
+    asm volatile("s_nop 4" : "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3]));
+  }
+  // G fragment (tap j, k half kh, row tile r) -> half j%2, rows 32r + lane%32 + j/2 (swizzled)
+  auto gbase0 = [&](int v) -> uint32_t {
+    const int ln = ck_lane();
+    const int jh = v >> 1, kh = v & 1;
+    const int row = (ln & 31) + jh;
+    return (uint32_t)(row * 64 + ck_phys(row, 2 * kh + (ln >> 5)) * 16);
+  };
+  auto block = [&](auto cbc) {
+    constexpr int CB = decltype(cbc)::value;
+    constexpr int SL = CB % 3, SL2 = (CB + 2) % 3;
+    uint32_t gb[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      gb[v] = gbase0(v) + SL * CH_SLAB;
+      asm volatile("" : "+v"(gb[v]));
+    }
+    auto gread = [&](int j, int kh, int r) -> chunk16 {
+      return *(const chunk16*)(smem + gb[(j >> 1) * 2 + kh] + (j & 1) * CH_HALF + r * 2048);
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    // DMA(CB) of every wave landed before the barrier (it is older than W(CB)[0])
+    if constexpr (CB == 0) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else if constexpr (CB < 7) asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");  // slot SL complete; slot SL2 (block CB-1) fully read
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t wlo = wlane(), dl = dlane();
+    chunk16 gf[4];
+    gf[0] = gread(0, 0, 0);
+    gf[1] = gread(0, 0, 1);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      // W(CB)[f] landed: vmcnt(19) (CB < 7; CB 0: everything but DMA(1) landed at the block start)
+      if constexpr (CB > 0 && CB < 7) {
+        if (f > 0) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+      } else if constexpr (CB == 7) {
+        constexpr int tab[8] = {19, 16, 13, 10, 7, 4, 2, 0};
+        if (f == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if (f == 2) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+        if (f == 3) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        if (f == 4) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        if (f == 5) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (f == 6) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        if (f == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        (void)tab;
+      }
+      const int j = f >> 1, kh = f & 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int n = f * 4 + r;  // fragment sequence: (f, r); two ahead
+        const int nn = n + 2;
+        if (nn < 32) gf[nn & 3] = gread((nn >> 2) >> 1, (nn >> 2) & 1, nn & 3);
+        ck_mfma(acc[0][r], W[f][0], gf[n & 3]);
+        ck_mfma(acc[1][r], W[f][1], gf[n & 3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // refill: the next block's fragment f (its MFMAs above were the last readers); then DMA piece f
+      if constexpr (CB < 7) {
+        // (an MFMA reads its A operand in its first passes; the loads land hundreds of cycles later)
+        wload(wlo, CB + 1, f, 0, W[f][0]);
+        wload(wlo, CB + 1, f, 1, W[f][1]);
+        if (f < 5) {
+          if constexpr (CB + 2 < 8) dma1(dl, CB + 2, SL2, f);
+          else dma1(dl, 7, SL2, f);  // count-keeping re-issue into slot 2 (read by no later block)
+        }
+      }
+    }
+  };
+  block(std::integral_constant<int, 0>{});
+  block(std::integral_constant<int, 1>{});
+  block(std::integral_constant<int, 2>{});
+  block(std::integral_constant<int, 3>{});
+  block(std::integral_constant<int, 4>{});
+  block(std::integral_constant<int, 5>{});
+  block(std::integral_constant<int, 6>{});
+  block(std::integral_constant<int, 7>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no load may land in a reused register)
+
+  // ---------------- epilogue: ChannelNorm (unbiased) over the 256 channels, ReLU, bf16
+  // lane holds C[row = 32r + lane%32][channel 64w + 32c + 8(e/4) + 4(lane/32) + e%4]
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+a"(acc[c][0]), "+a"(acc[c][1]), "+a"(acc[c][2]), "+a"(acc[c][3]));
+  auto val = [&](int c, int r, int q) -> f32x4 {
+    return f32x4{acc[c][r][4 * q], acc[c][r][4 * q + 1], acc[c][r][4 * q + 2], acc[c][r][4 * q + 3]};
+  };
+  // (mean, M2) per row and 32-channel group g = 2w + c, in the 256-row kernel's arithmetic (groups of
+  // 32, the same sums in the same order): the outputs are bit-identical to convk4_kernel's
+  float2* red = (float2*)(smem + CH_RED);  // [128 rows][8 groups]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const f32x4 t = (val(c, r, 0) + val(c, r, 1)) + (val(c, r, 2) + val(c, r, 3));
+      float sum = (t[0] + t[1]) + (t[2] + t[3]);
+      sum = ck_xsum(sum);
+      const float mw = sum * (1.0f / 32);
+      f32x4 sq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sq += val(c, r, q) * val(c, r, q);
+      float m2 = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+      m2 = fmaxf(ck_xsum(m2) - 32.0f * mw * mw, 0.f);
+      const int ln = ck_lane();
+      if (ln < 32) red[(r * 32 + ln) * 8 + 2 * w + c] = float2{mw, m2};
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  bf16* obase = a.out + (int64_t)s * a.out_seq_stride;
+  const __amdgpu_buffer_rsrc_t orsc = make_rsrc(obase, (uint32_t)((int64_t)a.M * 256 * 2));
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int ln = ck_lane();
+    const f32x4* rp = (const f32x4*)(red + (r * 32 + (ln & 31)) * 8);
+    const f32x4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];  // (mean, M2) of groups 0..7
+    const float m = (((r0[0] + r0[2]) + (r1[0] + r1[2])) + ((r2[0] + r2[2]) + (r3[0] + r3[2]))) * 0.125f;
+    auto dev = [&](float mw) { return (mw - m) * (mw - m); };
+    const float M2 = (((r0[1] + r0[3]) + (r1[1] + r1[3])) + ((r2[1] + r2[3]) + (r3[1] + r3[3]))) +
+                     32.0f * (((dev(r0[0]) + dev(r0[2])) + (dev(r1[0]) + dev(r1[2]))) +
+                              ((dev(r2[0]) + dev(r2[2])) + (dev(r3[0]) + dev(r3[2]))));
+    float rstd = __builtin_amdgcn_rsqf(M2 * (1.0f / 255) + 1e-5f);
+    float nmr = -m * rstd;
+    asm volatile("" : "+v"(rstd), "+v"(nmr));
+    const int t = t0 + r * 32 + (ln & 31);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint32_t pk[4][2];
+      const uint32_t pro = (uint32_t)((w * 64 + c * 32 + 4 * (ln >> 5)) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 gg = *(const f32x4*)((const unsigned char*)PR + 1024 + pro + 32 * q);
+        const f32x4 ee = *(const f32x4*)((const unsigned char*)PR + 2048 + pro + 32 * q);
+        const f32x4 v = (val(c, r, q) * rstd + nmr) * gg + ee;
+        pk[q][0] = ck_relu2(v[0], v[1]);
+        pk[q][1] = ck_relu2(v[2], v[3]);
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+          pk[2 * p][d] = sw[0];
+          pk[2 * p + 1][d] = sw[1];
+        }
+        const int col = w * 64 + c * 32 + 8 * (2 * p + (ln >> 5));
+        const u32x4 o = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+        buf_store16(orsc, t < a.M ? (uint32_t)((t * 256 + col) * 2) : 0xFFFFFFF0u, o);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
@@ -414,6 +665,12 @@ hipError_t launch_convk4(const ConvK4Args& a, int S, hipStream_t st) {
   // free beside the recurrence, a.grid_cap), which measured slower in the bench (conv2..4 1.75 vs
   // 1.50 ms per step): its next tile's block 0 waits for the epilogue stores and W(0), and static
   // striding balances worse than the dispatcher handing tiles to whichever CU frees up.
+  if (a.dbg == 0) {  // production: 128-row tiles, two workgroups per CU (convk4h_kernel)
+    const int ntb2 = (a.M + 127) / 128;
+    hipLaunchKernelGGL(convk4h_kernel, dim3(ntb2 * S), dim3(256), 0, st, a, ntb2);
+    return hipGetLastError();
+  }
+  // diagnostics builds (a.dbg != 0: tools/diag_convk4.py, stamps) run the 256-row kernel
   const dim3 grid(ntiles);
   switch (a.dbg) {
     case 0: hipLaunchKernelGGL(convk4_kernel<0>, grid, dim3(512), 0, st, a, ntb, ntiles); break;
