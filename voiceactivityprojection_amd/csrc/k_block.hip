@@ -36,6 +36,15 @@ constexpr int ROWB = D * 2;  // bf16 row of the panel / of a hidden slice: 512 B
 // cycles per SIMD, so 2 in flight leave the L2 round trip exposed; 8 in flight cost 48 VGPRs,
 // which drops the 64-row kernels from two workgroups per CU to one
 
+// weight prefetch depth (k-steps in flight) of the production instantiations: the block kernels sit at
+// 124 VGPRs (two workgroups per CU need <= 128), the LN-projection kernels at 90-100
+#ifndef BLK_NPF
+#define BLK_NPF 2
+#endif
+#ifndef LNP_NPF
+#define LNP_NPF 2
+#endif
+
 template <int MT> struct Blk {
   static constexpr int R = 16 * MT;
   static constexpr int OFF_H = R * ROWB;
@@ -457,15 +466,15 @@ hipError_t launch_mt(const BlockArgs& g, hipStream_t st) {
   static const bool stamps = getenv("VAP_BLOCK_STAMPS") != nullptr;
   if (g.np) {  // fused next-layer projections (the 64-row variant only: launch_block forces MT 4)
     if constexpr (MT == 4) {
-      if (g.nr) hipLaunchKernelGGL((block_kernel<MT, true, false, 2, 3, 2>), grid, dim3(512), 0, st, g);
-      else hipLaunchKernelGGL((block_kernel<MT, true, false, 2, 3, 0>), grid, dim3(512), 0, st, g);
+      if (g.nr) hipLaunchKernelGGL((block_kernel<MT, true, false, BLK_NPF, 3, 2>), grid, dim3(512), 0, st, g);
+      else hipLaunchKernelGGL((block_kernel<MT, true, false, BLK_NPF, 3, 0>), grid, dim3(512), 0, st, g);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
   }
   if (stamps && g.o) hipLaunchKernelGGL((block_kernel<MT, true, true>), grid, dim3(512), 0, st, g);
-  else if (g.o) hipLaunchKernelGGL((block_kernel<MT, true>), grid, dim3(512), 0, st, g);
-  else hipLaunchKernelGGL((block_kernel<MT, false>), grid, dim3(512), 0, st, g);
+  else if (g.o) hipLaunchKernelGGL((block_kernel<MT, true, false, BLK_NPF>), grid, dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((block_kernel<MT, false, false, BLK_NPF>), grid, dim3(512), 0, st, g);
   return hipGetLastError();
 }
 
@@ -698,9 +707,9 @@ hipError_t launch_lnproj_mt(const LnProjArgs& g, hipStream_t st) {
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0>), grid, dim3(512), 0, st, g);
-  else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0>), grid, dim3(512), 0, st, g);
-  else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2>), grid, dim3(512), 0, st, g);
+  if (g.o && g.np == 1 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, true, 1, 0, false, LNP_NPF>), grid, dim3(512), 0, st, g);
+  else if (!g.o && g.np == 3 && g.nr == 0) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 0, false, LNP_NPF>), grid, dim3(512), 0, st, g);
+  else if (!g.o && g.np == 3 && g.nr == 2) hipLaunchKernelGGL((lnproj_kernel<MT, false, 3, 2, false, LNP_NPF>), grid, dim3(512), 0, st, g);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
