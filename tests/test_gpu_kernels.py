@@ -138,6 +138,7 @@ def test_convk4(S, L_in, a, b):
     got = out.float().cpu()
     err = (got[:, :M] - ref).abs().max().item()
     assert err <= 3e-2 * max(1.0, ref.abs().max().item()), f"max err {err}"
+    assert bool((got[:, M:] == 7.0).all()), "rows past M were written"  # the tile's store guard
     assert torch.all(got[:, M:] == 7.0), "rows past the range were written"
 
 
